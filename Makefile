@@ -1,0 +1,50 @@
+# Build of the MI355X block-hash path (gfx950 only) and of the CPU oracle.
+#   make            -> ciruela_amd/libciruela_amd.so, bin/ciruela-index, oracle
+#   make oracle     -> oracle/build/liboracle_blake2b.so (test infrastructure)
+HIPCC ?= /opt/rocm/bin/hipcc
+CXX ?= g++
+CC ?= gcc
+ARCH ?= gfx950
+# COV5 keeps the code object loadable by the ROCm 7.0 runtime that ships
+# inside the PyTorch wheel as well as by /opt/rocm (7.2).
+COMMON := -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Iinclude -Iciruela_amd/csrc
+HIPFLAGS ?= $(COMMON) --offload-arch=$(ARCH) -mcode-object-version=5
+HOSTFLAGS ?= $(COMMON) -x c++ -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include
+CSRC := ciruela_amd/csrc
+OBJDIR := build/obj
+LIB := ciruela_amd/libciruela_amd.so
+CLI := bin/ciruela-index
+
+SRCS_HIP := $(CSRC)/kernels.hip
+SRCS_CPP := $(CSRC)/runtime.cpp $(CSRC)/dirsig.cpp $(CSRC)/scan.cpp $(CSRC)/registry.cpp
+OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS_HIP)) \
+        $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(SRCS_CPP))
+HDRS := $(wildcard $(CSRC)/*.hpp) include/ciruela_blockhash.h
+
+all: $(LIB) $(CLI) oracle
+
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# host-only translation units: compiled by hipcc as C++ (HIP headers, no device code)
+$(OBJDIR)/%.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HOSTFLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS) -lpthread
+
+$(CLI): $(CSRC)/cli.cpp $(LIB) $(HDRS)
+	@mkdir -p bin
+	$(HIPCC) $(HOSTFLAGS) $< -o $@ -Lciruela_amd -lciruela_amd \
+	    -Wl,-rpath,'$$ORIGIN/../ciruela_amd'
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf build $(LIB) $(CLI)
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean

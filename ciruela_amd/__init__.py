@@ -1,0 +1,470 @@
+"""ciruela_amd — MI355X-native block-indexing path of tailhook/ciruela.
+
+Python mirror of the reference's public interface for the indexing path,
+over the C ABI in include/ciruela_blockhash.h (libciruela_amd.so).  Names,
+argument meaning and error behaviour follow the reference:
+
+=============================  ==============================================
+this module                     reference (tailhook/ciruela v0.6.12)
+=============================  ==============================================
+BlockHash                       ciruela::blocks::BlockHash (src/block_id.rs:19)
+BlockHash.hash_bytes            BlockHash::hash_bytes (src/block_id.rs:37-43)
+ImageId                         ciruela::index::ImageId (src/id.rs:142)
+HashType                        dir_signature::HashType (external 0.2.9)
+Hashes.hash_file                dir_signature::v1::Hashes::hash_file
+ScannerConfig, v1.scan          dir_signature::{ScannerConfig, v1::scan}
+                                (src/client/sync/uploads.rs:49-59)
+get_hash                        dir_signature::get_hash (src/index.rs:99)
+InMemoryIndexes                 ciruela::index::InMemoryIndexes (src/index.rs:53)
+ThreadedBlockReader             ciruela::blocks::ThreadedBlockReader
+                                (src/blocks.rs:85)
+=============================  ==============================================
+
+All hashing runs on gfx950 through the library; there is no CPU fallback.
+"""
+import ctypes
+import os
+import threading
+
+from . import _native as _n
+from ._native import CiruelaError, NoDevice  # noqa: F401
+
+__all__ = [
+    "BlockHash", "ImageId", "HashType", "Hashes", "ScannerConfig", "v1", "get_hash",
+    "InMemoryIndexes", "ThreadedBlockReader", "BlockHint", "Context", "default_context",
+    "IndexError_", "DirError", "ReadError", "CiruelaError", "NoDevice",
+]
+
+DEFAULT_BLOCK_SIZE = 32768
+
+
+def _buf(data):
+    """(pointer, keepalive) for a bytes-like object."""
+    if isinstance(data, (bytes, bytearray, memoryview)):
+        mv = memoryview(data).cast("B")
+        n = mv.nbytes
+        if n == 0:
+            return None, b""
+        if mv.readonly:
+            arr = (ctypes.c_char * n).from_buffer_copy(mv)
+        else:
+            arr = (ctypes.c_char * n).from_buffer(mv)
+        return ctypes.cast(arr, ctypes.c_void_p), arr
+    raise TypeError("expected a bytes-like object, got %r" % type(data))
+
+
+class Context:
+    """A cir_ctx: the devices the host-memory entry points run on."""
+
+    def __init__(self, device_mask=0, staging_bytes=0):
+        h = ctypes.c_void_p()
+        _n.check(_n.lib.cir_init(ctypes.byref(h), device_mask, staging_bytes))
+        self._h = h
+
+    @property
+    def handle(self):
+        return self._h
+
+    def devices(self):
+        ids = (ctypes.c_int * 64)()
+        n = _n.lib.cir_ctx_devices(self._h, ids, 64)
+        return list(ids[:n])
+
+    def close(self):
+        if self._h:
+            _n.lib.cir_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- device-resident entry points (pointers are device addresses) ----
+    def hash_chunks_dev(self, d_data, nbytes, block_size, d_out, stream=0):
+        _n.check(_n.lib.cir_hash_chunks_dev(self._h, d_data, nbytes, block_size, d_out, stream))
+
+    def hash_blocks_dev(self, d_arena, d_off, d_len, nblk, d_out, stream=0):
+        _n.check(_n.lib.cir_hash_blocks_dev(self._h, d_arena, d_off, d_len, nblk, d_out, stream))
+
+    # ---- host-memory entry points ----------------------------------------
+    def hash_blocks(self, arena, offsets, lengths):
+        """Digests (n x 32 bytes) of arena[off[i] : off[i] + len[i]]."""
+        n = len(offsets)
+        if len(lengths) != n:
+            raise ValueError("offsets and lengths differ in length")
+        for o, ln in zip(offsets, lengths):
+            if o < 0 or ln < 0 or o + ln > len(arena):
+                raise ValueError("block outside the arena")
+        out = ctypes.create_string_buffer(32 * max(n, 1))
+        if n == 0:
+            return b""
+        offs = (ctypes.c_uint64 * n)(*offsets)
+        lens = (ctypes.c_uint32 * n)(*lengths)
+        ptr, keep = _buf(arena) if len(arena) else (ctypes.c_void_p(0), None)
+        if ptr is None:
+            one = ctypes.create_string_buffer(1)
+            ptr, keep = ctypes.cast(one, ctypes.c_void_p), one
+        _n.check(_n.lib.cir_hash_blocks(self._h, ptr, offs, lens, n, out))
+        del keep
+        return out.raw[:32 * n]
+
+    def hash_file(self, fd, block_size):
+        size = ctypes.c_uint64()
+        hp = ctypes.c_void_p()
+        nh = ctypes.c_size_t()
+        _n.check(_n.lib.cir_hash_file(self._h, fd, block_size, ctypes.byref(size),
+                                      ctypes.byref(hp), ctypes.byref(nh)))
+        return size.value, _n.take_buffer(hp.value, 32 * nh.value)
+
+    def hash_memory(self, data, block_size):
+        ptr, keep = _buf(data)
+        hp = ctypes.c_void_p()
+        nh = ctypes.c_size_t()
+        _n.check(_n.lib.cir_hash_memory(self._h, ptr, len(data), block_size, ctypes.byref(hp),
+                                        ctypes.byref(nh)))
+        del keep
+        return _n.take_buffer(hp.value, 32 * nh.value)
+
+    def scan(self, config):
+        dirs = [os.fsencode(d) for d, _ in config._dirs]
+        pres = [p.encode() for _, p in config._dirs]
+        cd = (ctypes.c_char_p * len(dirs))(*dirs)
+        cp = (ctypes.c_char_p * len(pres))(*pres)
+        out = ctypes.c_void_p()
+        ln = ctypes.c_size_t()
+        _n.check(_n.lib.cir_scan_v1(self._h, cd, cp, len(dirs), config._block_size,
+                                    config._hash.code, config._threads, ctypes.byref(out),
+                                    ctypes.byref(ln)))
+        return _n.take_buffer(out.value, ln.value)
+
+    def index_rewrite(self, data):
+        ptr, keep = _buf(data)
+        out = ctypes.c_void_p()
+        ln = ctypes.c_size_t()
+        _n.check(_n.lib.cir_index_rewrite(self._h, ptr, len(data), ctypes.byref(out),
+                                          ctypes.byref(ln)))
+        del keep
+        return _n.take_buffer(out.value, ln.value)
+
+
+_default = None
+_default_lock = threading.Lock()
+
+
+def default_context():
+    """Process-wide context on every visible device (created on first use)."""
+    global _default
+    with _default_lock:
+        if _default is None:
+            _default = Context()
+        return _default
+
+
+def _hex(b):
+    return b.hex()
+
+
+class BlockHash:
+    """32-byte block id (src/block_id.rs:19); displays as lowercase hex."""
+
+    __slots__ = ("_b",)
+
+    def __init__(self, raw):
+        if len(raw) != 32:
+            raise ValueError("BlockHash is 32 bytes")
+        self._b = bytes(raw)
+
+    @staticmethod
+    def from_bytes(raw):
+        """Some(BlockHash) for 32 bytes, None otherwise (src/block_id.rs:28-35)."""
+        return BlockHash(raw) if len(raw) == 32 else None
+
+    @staticmethod
+    def hash_bytes(data):
+        """BLAKE2b-256 of data, on the GPU (src/block_id.rs:37-43)."""
+        ptr, keep = _buf(bytes(data)) if len(data) else (None, None)
+        out = ctypes.create_string_buffer(32)
+        _n.check(_n.lib.cir_blake2b256(ptr, len(data), out))
+        del keep
+        return BlockHash(out.raw)
+
+    def __bytes__(self):
+        return self._b
+
+    def __eq__(self, other):
+        return isinstance(other, BlockHash) and other._b == self._b
+
+    def __hash__(self):
+        return hash(self._b)
+
+    def __str__(self):
+        return _hex(self._b)
+
+    def __repr__(self):
+        return "BlockHash(%s)" % _hex(self._b)
+
+
+class ImageId:
+    """Image id = the hash on the index's last line (src/id.rs:142-217)."""
+
+    __slots__ = ("_b",)
+
+    def __init__(self, raw):
+        self._b = bytes(raw)
+
+    @staticmethod
+    def from_str(s):
+        try:
+            return ImageId(bytes.fromhex(s))
+        except ValueError:
+            raise ValueError("errors parding hexadecimal image id")
+
+    def __bytes__(self):
+        return self._b
+
+    def __eq__(self, other):
+        return isinstance(other, ImageId) and other._b == self._b
+
+    def __hash__(self):
+        return hash(self._b)
+
+    def __str__(self):
+        return _hex(self._b)
+
+    def __repr__(self):
+        return "ImageId(%s)" % _hex(self._b)
+
+
+class HashType:
+    """dir_signature::HashType."""
+
+    __slots__ = ("code", "name")
+
+    def __init__(self, code, name):
+        self.code = code
+        self.name = name
+
+    @staticmethod
+    def blake2b_256():
+        return HashType(_n.CIR_HASH_BLAKE2B_256, "blake2b/256")
+
+    @staticmethod
+    def sha512_256():
+        return HashType(_n.CIR_HASH_SHA512_256, "sha512/256")
+
+    def __eq__(self, other):
+        return isinstance(other, HashType) and other.code == self.code
+
+    def __repr__(self):
+        return "HashType(%s)" % self.name
+
+
+class Hashes:
+    """Per-block hashes of one file (dir_signature::v1::Hashes)."""
+
+    def __init__(self, raw, block_size, hash_type=None):
+        self._raw = bytes(raw)
+        self._bs = block_size
+        self._ht = hash_type or HashType.blake2b_256()
+
+    @staticmethod
+    def hash_file(hash_type, block_size, reader, context=None):
+        """(size, Hashes) of everything `reader` yields (src/blocks.rs:193).
+
+        reader: an int fd, an object with fileno(), or bytes-like data.
+        """
+        if hash_type.code != _n.CIR_HASH_BLAKE2B_256:
+            raise CiruelaError(_n.CIR_EUNSUPPORTED, "only blake2b/256 runs on the GPU")
+        ctx = context or default_context()
+        if isinstance(reader, (bytes, bytearray, memoryview)):
+            raw = ctx.hash_memory(reader, block_size)
+            return len(reader), Hashes(raw, block_size, hash_type)
+        fd = reader if isinstance(reader, int) else reader.fileno()
+        size, raw = ctx.hash_file(fd, block_size)
+        return size, Hashes(raw, block_size, hash_type)
+
+    def __len__(self):
+        return len(self._raw) // 32
+
+    def get(self, i):
+        return self._raw[32 * i:32 * i + 32]
+
+    def __iter__(self):
+        return (self.get(i) for i in range(len(self)))
+
+    def block_size(self):
+        return self._bs
+
+    def raw(self):
+        return self._raw
+
+
+class ScannerConfig:
+    """dir_signature::ScannerConfig (used at src/client/sync/uploads.rs:50-54)."""
+
+    def __init__(self):
+        self._threads = 4  # GlobalOptions.threads default (src/client/global_options.rs:13)
+        self._hash = HashType.blake2b_256()
+        self._dirs = []
+        self._block_size = DEFAULT_BLOCK_SIZE
+        self._progress = False
+
+    @staticmethod
+    def new():
+        return ScannerConfig()
+
+    def threads(self, n):
+        self._threads = int(n)
+        return self
+
+    def auto_threads(self):
+        self._threads = 0
+        return self
+
+    def hash(self, hash_type):
+        self._hash = hash_type
+        return self
+
+    def block_size(self, n):
+        self._block_size = int(n)
+        return self
+
+    def add_dir(self, path, prefix="/"):
+        self._dirs.append((os.fspath(path), prefix))
+        return self
+
+    def print_progress(self):
+        self._progress = True
+        return self
+
+
+class v1:  # noqa: N801 - mirrors the `dir_signature::v1` module
+    @staticmethod
+    def scan(config, out=None, context=None):
+        """dir_signature::v1::scan(&cfg, &mut Vec<u8>): index bytes.
+
+        Like the reference, appends to `out` (a bytearray) when given."""
+        data = (context or default_context()).scan(config)
+        if out is not None:
+            out.extend(data)
+        return data
+
+
+def get_hash(index):
+    """dir_signature::get_hash: the id bytes on the index's last line."""
+    ptr, keep = _buf(index) if len(index) else (None, None)
+    out = ctypes.create_string_buffer(64)
+    n = ctypes.c_size_t()
+    _n.check(_n.lib.cir_index_get_hash(ptr, len(index), out, ctypes.byref(n)))
+    del keep
+    return out.raw[:n.value]
+
+
+class IndexError_(CiruelaError):  # noqa: N801 - ciruela::index::IndexError
+    pass
+
+
+class DirError(CiruelaError):
+    """ciruela::blocks::DirError (src/blocks.rs:114-127)."""
+
+
+class ReadError(CiruelaError):
+    """ReadError of src/index.rs:74-85 / src/blocks.rs:95-111."""
+
+
+def _raise_as(cls, fn):
+    try:
+        fn()
+    except CiruelaError as e:
+        raise cls(e.status, e.detail) from None
+
+
+class InMemoryIndexes:
+    """GetIndex implementation serving indexes from memory (src/index.rs:53)."""
+
+    def __init__(self):
+        self._h = _n.lib.cir_indexes_new()
+
+    def __del__(self):
+        try:
+            _n.lib.cir_indexes_free(self._h)
+        except Exception:
+            pass
+
+    def register_index(self, data):
+        """Returns the ImageId (src/index.rs:98-105); IndexError_ on parse failure."""
+        ptr, keep = _buf(bytes(data)) if len(data) else (ctypes.c_void_p(1), None)
+        out = ctypes.create_string_buffer(64)
+        n = ctypes.c_size_t()
+        _raise_as(IndexError_, lambda: _n.check(
+            _n.lib.cir_indexes_register(self._h, ptr, len(data), out, ctypes.byref(n))))
+        del keep
+        return ImageId(out.raw[:n.value])
+
+    def read_index(self, image_id):
+        raw = bytes(image_id)
+        p = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        _raise_as(ReadError, lambda: _n.check(
+            _n.lib.cir_indexes_read(self._h, raw, len(raw), ctypes.byref(p), ctypes.byref(n))))
+        return _n.take_buffer(p.value, n.value)
+
+
+class BlockHint:
+    """src/blocks.rs:46-48 (currently always empty)."""
+
+    @staticmethod
+    def empty():
+        return BlockHint()
+
+
+class ThreadedBlockReader:
+    """GetBlock implementation (src/blocks.rs:85-240)."""
+
+    def __init__(self, num_threads=40):
+        self._h = _n.lib.cir_blocks_new()
+        self._threads = num_threads
+
+    @staticmethod
+    def new():
+        return ThreadedBlockReader()
+
+    @staticmethod
+    def new_num_threads(num):
+        return ThreadedBlockReader(num)
+
+    def __del__(self):
+        try:
+            _n.lib.cir_blocks_free(self._h)
+        except Exception:
+            pass
+
+    def __len__(self):
+        return _n.lib.cir_blocks_len(self._h)
+
+    def register_dir(self, dir, index_data):  # noqa: A002 - reference name
+        ptr, keep = _buf(bytes(index_data)) if len(index_data) else (ctypes.c_void_p(1), None)
+        _raise_as(DirError, lambda: _n.check(_n.lib.cir_blocks_register_dir(
+            self._h, os.fsencode(dir), ptr, len(index_data))))
+        del keep
+
+    def register_memory_blocks(self, hash_type, block_size, data, context=None):
+        if hash_type.code != _n.CIR_HASH_BLAKE2B_256:
+            raise CiruelaError(_n.CIR_EUNSUPPORTED, "only blake2b/256 runs on the GPU")
+        ctx = context or default_context()
+        ptr, keep = _buf(bytes(data)) if len(data) else (None, None)
+        _n.check(_n.lib.cir_blocks_register_memory(ctx.handle, self._h, ptr, len(data),
+                                                   block_size))
+        del keep
+
+    def read_block(self, block_hash, hint=None):
+        raw = bytes(block_hash)
+        if len(raw) != 32:
+            raise ValueError("BlockHash is 32 bytes")
+        p = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        _raise_as(ReadError, lambda: _n.check(
+            _n.lib.cir_blocks_read(self._h, raw, ctypes.byref(p), ctypes.byref(n))))
+        return _n.take_buffer(p.value, n.value)

@@ -1,0 +1,193 @@
+// BLAKE2b-256 (RFC 7693, unkeyed, nn = 32) device core for gfx950.
+//
+// Replaces the compression function of the `blake2 0.7.1` crate that
+// ciruela reaches through `BlockHash::hash_bytes` (reference
+// src/block_id.rs:37-43: `Blake2b::VariableOutput::new(32)`, `input`,
+// `variable_result`) and through dir-signature's per-block hashing
+// (`Hashes::hash_file`, called at src/blocks.rs:193).
+//
+// Mapping (DESIGN.md "Kernels"): one block chain per lane.  A BLAKE2b chain
+// is strictly sequential (ceil(len/128) compressions), so parallelism is
+// across blocks; each lane keeps the whole 16-word working vector, the
+// 8-word chain value and the current + next 128-byte message line in VGPRs.
+//
+// Arithmetic on CDNA4's 32-bit VALU:
+//   * 64-bit adds      -> v_lshl_add_u64 (shift 0)
+//   * xor + rotr 32    -> 2 x v_xor_b32, the rotate is a register swap
+//   * xor + rotr 24/16 -> 2 x v_xor_b32 + 2 x v_alignbit_b32
+//   * xor + rotr 63    -> 2 x v_xor_b32 + 2 x v_alignbit_b32 (swap + 31)
+// hipcc lowers a plain u64 rotate to 64-bit shifts + or (5 ops), so the
+// rotates are written on 32-bit halves with __builtin_amdgcn_alignbit.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cir {
+namespace dev {
+
+__device__ __forceinline__ uint32_t lo32(uint64_t x) { return (uint32_t)x; }
+__device__ __forceinline__ uint32_t hi32(uint64_t x) { return (uint32_t)(x >> 32); }
+__device__ __forceinline__ uint64_t mk64(uint32_t lo, uint32_t hi) {
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// rotr64(a ^ b, N) on 32-bit halves.
+template <int N>
+__device__ __forceinline__ uint64_t xor_rotr(uint64_t a, uint64_t b) {
+  const uint32_t l = lo32(a) ^ lo32(b), h = hi32(a) ^ hi32(b);
+  if constexpr (N == 32) {
+    return mk64(h, l);
+  } else if constexpr (N < 32) {
+    return mk64(__builtin_amdgcn_alignbit(h, l, N), __builtin_amdgcn_alignbit(l, h, N));
+  } else {
+    return mk64(__builtin_amdgcn_alignbit(l, h, N - 32), __builtin_amdgcn_alignbit(h, l, N - 32));
+  }
+}
+
+#define CIR_IV0 0x6a09e667f3bcc908ULL
+#define CIR_IV1 0xbb67ae8584caa73bULL
+#define CIR_IV2 0x3c6ef372fe94f82bULL
+#define CIR_IV3 0xa54ff53a5f1d36f1ULL
+#define CIR_IV4 0x510e527fade682d1ULL
+#define CIR_IV5 0x9b05688c2b3e6c1fULL
+#define CIR_IV6 0x1f83d9abfb41bd6bULL
+#define CIR_IV7 0x5be0cd19137e2179ULL
+// Parameter block word 0 for digest_length = 32, key_length = 0,
+// fanout = 1, depth = 1 (RFC 7693 section 2.5).
+#define CIR_P0_256 0x01010020ULL
+
+#define CIR_G(a, b, c, d, x, y)   \
+  a = a + b + (x);                \
+  d = xor_rotr<32>(d, a);         \
+  c = c + d;                      \
+  b = xor_rotr<24>(b, c);         \
+  a = a + b + (y);                \
+  d = xor_rotr<16>(d, a);         \
+  c = c + d;                      \
+  b = xor_rotr<63>(b, c);
+
+#define CIR_ROUND(s0, s1, s2, s3, s4, s5, s6, s7, s8, s9, s10, s11, s12, s13, s14, s15) \
+  CIR_G(v0, v4, v8, v12, m[s0], m[s1])                                                   \
+  CIR_G(v1, v5, v9, v13, m[s2], m[s3])                                                   \
+  CIR_G(v2, v6, v10, v14, m[s4], m[s5])                                                  \
+  CIR_G(v3, v7, v11, v15, m[s6], m[s7])                                                  \
+  CIR_G(v0, v5, v10, v15, m[s8], m[s9])                                                  \
+  CIR_G(v1, v6, v11, v12, m[s10], m[s11])                                                \
+  CIR_G(v2, v7, v8, v13, m[s12], m[s13])                                                 \
+  CIR_G(v3, v4, v9, v14, m[s14], m[s15])
+
+// F(h, m, t, f) of RFC 7693 section 3.2 with t < 2^64 (t[1] == 0: a block
+// is at most 2^32 bytes here) and f0 = last ? ~0 : 0, f1 = 0.
+__device__ __forceinline__ void compress(uint64_t h[8], const uint64_t m[16], uint64_t t,
+                                         bool last) {
+  uint64_t v0 = h[0], v1 = h[1], v2 = h[2], v3 = h[3];
+  uint64_t v4 = h[4], v5 = h[5], v6 = h[6], v7 = h[7];
+  uint64_t v8 = CIR_IV0, v9 = CIR_IV1, v10 = CIR_IV2, v11 = CIR_IV3;
+  uint64_t v12 = CIR_IV4 ^ t, v13 = CIR_IV5;
+  uint64_t v14 = last ? ~CIR_IV6 : CIR_IV6, v15 = CIR_IV7;
+  CIR_ROUND(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
+  CIR_ROUND(14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3)
+  CIR_ROUND(11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4)
+  CIR_ROUND(7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8)
+  CIR_ROUND(9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13)
+  CIR_ROUND(2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9)
+  CIR_ROUND(12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11)
+  CIR_ROUND(13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10)
+  CIR_ROUND(6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5)
+  CIR_ROUND(10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0)
+  CIR_ROUND(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
+  CIR_ROUND(14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3)
+  h[0] ^= v0 ^ v8;
+  h[1] ^= v1 ^ v9;
+  h[2] ^= v2 ^ v10;
+  h[3] ^= v3 ^ v11;
+  h[4] ^= v4 ^ v12;
+  h[5] ^= v5 ^ v13;
+  h[6] ^= v6 ^ v14;
+  h[7] ^= v7 ^ v15;
+}
+
+__device__ __forceinline__ void init_state(uint64_t h[8]) {
+  h[0] = CIR_IV0 ^ CIR_P0_256;
+  h[1] = CIR_IV1;
+  h[2] = CIR_IV2;
+  h[3] = CIR_IV3;
+  h[4] = CIR_IV4;
+  h[5] = CIR_IV5;
+  h[6] = CIR_IV6;
+  h[7] = CIR_IV7;
+}
+
+// One full 128-byte message line, 16-byte aligned: 8 x global_load_dwordx4.
+__device__ __forceinline__ void load_line16(uint64_t m[16], const uint8_t* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint4 x = q[k];
+    m[2 * k] = mk64(x.x, x.y);
+    m[2 * k + 1] = mk64(x.z, x.w);
+  }
+}
+
+// The first n (0..128) bytes of a line at any alignment, zero padded
+// (RFC 7693: the last block is padded with zeros).  Never reads past p + n.
+// Used for ragged tails and misaligned blocks only.
+__device__ __forceinline__ void load_line_safe(uint64_t m[16], const uint8_t* p, uint32_t n) {
+  const bool al4 = (reinterpret_cast<uintptr_t>(p) & 3u) == 0;
+#pragma unroll
+  for (int w = 0; w < 32; ++w) {
+    uint32_t x = 0;
+    const uint32_t b0 = 4u * w;
+    if (al4 && b0 + 4u <= n) {
+      x = *reinterpret_cast<const uint32_t*>(p + b0);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (b0 + k < n) x |= (uint32_t)p[b0 + k] << (8 * k);
+    }
+    if (w & 1)
+      m[w >> 1] |= (uint64_t)x << 32;
+    else
+      m[w >> 1] = x;
+  }
+}
+
+// Line i of a chain over [p, p + len): full lines use the vector loader when
+// the chain start is 16-byte aligned, the rest go through the safe loader.
+__device__ __forceinline__ void load_line_any(uint64_t m[16], const uint8_t* p, uint64_t i,
+                                              uint64_t nfull, uint32_t rem, bool al16) {
+  const uint8_t* q = p + (i << 7);
+  if (al16 && i < nfull)
+    load_line16(m, q);
+  else
+    load_line_safe(m, q, i < nfull ? 128u : rem);
+}
+
+// Digest of one chain (a block of len bytes at p) into h[0..3].
+// Compressions: max(1, ceil(len / 128)); the last one carries the final flag
+// and t = len (an exact multiple of 128 is compressed as final, not followed
+// by an empty block; the empty input is one all-zero final block, t = 0).
+// General path (ragged lengths, any alignment): one message buffer, no
+// prefetch, so it stays under the 128-VGPR budget of 4 waves per SIMD.
+__device__ __forceinline__ void hash_chain(const uint8_t* p, uint64_t len, uint64_t h[8]) {
+  init_state(h);
+  const uint32_t nfull = (uint32_t)(len >> 7);
+  const uint32_t rem = (uint32_t)(len & 127u);
+  const uint32_t total = nfull + ((rem != 0u || len == 0) ? 1u : 0u);
+  const bool al16 = (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+  uint64_t m[16];
+  for (uint32_t i = 0; i < total; ++i) {
+    load_line_any(m, p, i, nfull, rem, al16);
+    const bool last = i + 1 == total;
+    compress(h, m, last ? len : (uint64_t)(i + 1) << 7, last);
+  }
+}
+
+__device__ __forceinline__ void store_digest(uint8_t* out, const uint64_t h[8]) {
+  uint4* o = reinterpret_cast<uint4*>(out);
+  o[0] = make_uint4(lo32(h[0]), hi32(h[0]), lo32(h[1]), hi32(h[1]));
+  o[1] = make_uint4(lo32(h[2]), hi32(h[2]), lo32(h[3]), hi32(h[3]));
+}
+
+}  // namespace dev
+}  // namespace cir

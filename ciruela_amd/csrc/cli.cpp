@@ -1,0 +1,170 @@
+// ciruela-index: the indexing half of `ciruela sync`, on the GPU path.
+//
+// Reference: `ciruela sync` (src/client/main.rs:94-99 -> src/client/sync/
+// mod.rs:168-220 -> uploads::prepare, src/client/sync/uploads.rs:61-105).
+// For every --append / --append-weak / --replace SRC:DEST it runs the scan
+// (uploads.rs:49-59, threads = --disk-threads, default 4), registers the
+// index (InMemoryIndexes::register_index -> ImageId) and prints
+//   <image id> <kind> <dest> <src>
+// Signing and the upload itself (networking, src/client/sync/network.rs) are
+// out of scope; --index-dir writes each index as
+// <dir>/<image id>.ds1 so a separate uploader can pick it up.
+//
+//   ciruela-index sync [--disk-threads N] [--block-size N] [--index-dir D]
+//                      --append SRC:/DEST [--append-weak SRC:/DEST]
+//                      [--replace SRC:/DEST[:OLD_IMAGE_ID]] ...
+//   ciruela-index hash [--block-size N] FILE...   (per-block BlockHash list)
+#include <fcntl.h>
+#include <stdio.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <string>
+#include <vector>
+
+#include "ciruela_blockhash.h"
+
+static void usage() {
+  fprintf(stderr,
+          "usage: ciruela-index sync [--disk-threads N] [--block-size N] [--index-dir D]\n"
+          "                          (--append|--append-weak|--replace) SRC:/DEST ...\n"
+          "       ciruela-index hash [--block-size N] FILE...\n");
+}
+
+static std::string hex(const uint8_t* p, size_t n) {
+  static const char k[] = "0123456789abcdef";
+  std::string s;
+  for (size_t i = 0; i < n; ++i) {
+    s += k[p[i] >> 4];
+    s += k[p[i] & 15];
+  }
+  return s;
+}
+
+static int die(int rc, const char* what) {
+  fprintf(stderr, "%s: %s: %s\n", what, cir_strerror(rc), cir_last_error());
+  return rc == CIR_EIO ? 1 : 2;
+}
+
+struct Job {
+  std::string kind, src, dest;
+};
+
+// split "source:/dir/dest" (src/client/sync/uploads.rs:25-33)
+static bool split(const std::string& cli, std::string* src, std::string* dest) {
+  const size_t c = cli.find(':');
+  if (c == std::string::npos) return false;
+  *src = cli.substr(0, c);
+  std::string rest = cli.substr(c + 1);
+  const size_t c2 = rest.find(':');
+  *dest = c2 == std::string::npos ? rest : rest.substr(0, c2);
+  return !dest->empty() && (*dest)[0] == '/';
+}
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    usage();
+    return 2;
+  }
+  const std::string cmd = argv[1];
+  uint32_t threads = 4;  // GlobalOptions.threads (src/client/global_options.rs:13)
+  uint64_t bs = CIR_DEFAULT_BLOCK_SIZE;
+  std::string index_dir;
+  std::vector<Job> jobs;
+  std::vector<std::string> files;
+  for (int i = 2; i < argc; ++i) {
+    const std::string a = argv[i];
+    auto val = [&]() -> std::string {
+      if (i + 1 >= argc) {
+        usage();
+        exit(2);
+      }
+      return argv[++i];
+    };
+    if (a == "--disk-threads") threads = (uint32_t)std::stoul(val());
+    else if (a == "--block-size") bs = std::stoull(val());
+    else if (a == "--index-dir") index_dir = val();
+    else if (a == "--append" || a == "--append-weak" || a == "--replace") {
+      Job j;
+      j.kind = a.substr(2);
+      if (!split(val(), &j.src, &j.dest)) {
+        fprintf(stderr, "Destination directory is invalid, must be `source:/dir/dest`\n");
+        return 2;
+      }
+      jobs.push_back(j);
+    } else if (cmd == "hash" && a.size() && a[0] != '-') {
+      files.push_back(a);
+    } else {
+      usage();
+      return 2;
+    }
+  }
+  cir_ctx* ctx = nullptr;
+  int rc = cir_init(&ctx, 0, 0);
+  if (rc) return die(rc, "cir_init");
+  if (cmd == "hash") {
+    for (const std::string& f : files) {
+      const int fd = open(f.c_str(), O_RDONLY);
+      if (fd < 0) {
+        perror(f.c_str());
+        return 1;
+      }
+      uint64_t size = 0;
+      uint8_t* h = nullptr;
+      size_t n = 0;
+      rc = cir_hash_file(ctx, fd, bs, &size, &h, &n);
+      close(fd);
+      if (rc) return die(rc, f.c_str());
+      printf("%s %llu", f.c_str(), (unsigned long long)size);
+      for (size_t k = 0; k < n; ++k) printf(" %s", hex(h + 32 * k, 32).c_str());
+      printf("\n");
+      cir_free(h);
+    }
+  } else if (cmd == "sync") {
+    if (jobs.empty()) {
+      usage();
+      return 2;
+    }
+    cir_indexes* idx = cir_indexes_new();
+    cir_blocks* blocks = cir_blocks_new();
+    for (const Job& j : jobs) {
+      const auto t0 = std::chrono::steady_clock::now();
+      const char* dirs[1] = {j.src.c_str()};
+      const char* pre[1] = {"/"};
+      uint8_t* index = nullptr;
+      size_t len = 0;
+      rc = cir_scan_v1(ctx, dirs, pre, 1, bs, CIR_HASH_BLAKE2B_256, threads, &index, &len);
+      if (rc) return die(rc, ("error indexing dir " + j.src).c_str());
+      uint8_t id[64];
+      size_t idl = 0;
+      rc = cir_indexes_register(idx, index, len, id, &idl);
+      if (rc) return die(rc, "register_index");
+      rc = cir_blocks_register_dir(blocks, j.src.c_str(), index, len);
+      if (rc) return die(rc, "register_dir");
+      const double s =
+          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      printf("%s %s %s %s\n", hex(id, idl).c_str(), j.kind.c_str(), j.dest.c_str(),
+             j.src.c_str());
+      fprintf(stderr, "Indexed %s (%zu index bytes, %zu blocks) in %.3f s\n", j.src.c_str(), len,
+              cir_blocks_len(blocks), s);
+      if (!index_dir.empty()) {
+        const std::string p = index_dir + "/" + hex(id, idl) + ".ds1";
+        FILE* f = fopen(p.c_str(), "wb");
+        if (!f || fwrite(index, 1, len, f) != len) {
+          perror(p.c_str());
+          return 1;
+        }
+        fclose(f);
+      }
+      cir_free(index);
+    }
+    cir_blocks_free(blocks);
+    cir_indexes_free(idx);
+  } else {
+    usage();
+    return 2;
+  }
+  cir_destroy(ctx);
+  return 0;
+}

@@ -1,0 +1,88 @@
+// DIRSIGNATURE.v1 index format: emitter and parser (host C++).
+//
+// Restates what ciruela takes from the external crate dir-signature 0.2.9
+// (Cargo.toml:35; not vendored in the reference):
+//   * v1::Emitter  — used by MutableIndex::to_raw_data
+//                    (src/cluster/download.rs:266-276, dir order :287-319)
+//   * v1::Parser   — used by ThreadedBlockReader::register_dir
+//                    (src/blocks.rs:150-183) and RawIndex::into_mut
+//   * get_hash     — InMemoryIndexes::register_index (src/index.rs:98-105)
+// Pinned by the reference's only index fixture (src/cluster/download.rs:
+// 357-366): header line, "/dir" lines, "  name f size hex..." entries, an
+// empty file carries no hashes, footer = H(every byte after the header line).
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace cir {
+namespace dirsig {
+
+enum class HashType { kBlake2b256 = 1, kSha512_256 = 2 };
+
+const char* hash_type_name(HashType t);           // "blake2b/256", "sha512/256"
+bool parse_hash_type(const std::string& s, HashType* t);
+
+// dir-signature escapes bytes outside printable ASCII, the space and the
+// backslash as \xNN (lowercase hex).  Unverified against the crate (see
+// DESIGN.md "Index format"); consistent with every fixture in the reference.
+std::string escape(const std::string& raw);
+bool unescape(const std::string& esc, std::string* raw);
+
+std::string to_hex(const uint8_t* p, size_t n);
+bool from_hex(const std::string& s, std::vector<uint8_t>* out);
+
+struct Header {
+  HashType hash = HashType::kBlake2b256;
+  uint64_t block_size = 32768;
+};
+
+// Streaming emitter: header, then for each directory start_dir + entries;
+// finish() needs the footer digest of body() (computed by the caller on
+// the GPU) and appends its hex line.
+class Emitter {
+ public:
+  explicit Emitter(const Header& h);
+  void start_dir(const std::string& vpath);  // "/" or "/a/b" (raw bytes)
+  void add_file(const std::string& name, bool exe, uint64_t size, const uint8_t* hashes,
+                size_t nhash);
+  void add_symlink(const std::string& name, const std::string& target);
+  // Bytes the footer hashes: everything after the header line.
+  const std::string& body() const { return body_; }
+  std::string finish(const uint8_t* footer, size_t footer_len) const;
+  const std::string& header_line() const { return header_; }
+
+ private:
+  std::string header_;
+  std::string body_;
+};
+
+enum class EntryKind { kDir, kFile, kLink };
+
+struct Entry {
+  EntryKind kind;
+  std::string path;  // kDir: directory path; kFile/kLink: full path (dir + "/" + name)
+  bool exe = false;
+  uint64_t size = 0;
+  std::vector<uint8_t> hashes;  // nhash x digest_len
+  std::string target;           // kLink
+};
+
+struct Index {
+  Header header;
+  std::vector<Entry> entries;
+  std::vector<uint8_t> footer;  // decoded last line
+};
+
+// Parse a whole index.  Returns false with *err set on malformed input
+// (the reference's v1::ParseError).
+bool parse(const uint8_t* data, size_t len, Index* out, std::string* err);
+
+// dir_signature::get_hash: decode the hex on the last line.
+bool get_hash(const uint8_t* data, size_t len, std::vector<uint8_t>* id, std::string* err);
+
+size_t digest_len(HashType t);
+
+}  // namespace dirsig
+}  // namespace cir

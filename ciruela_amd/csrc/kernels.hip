@@ -1,0 +1,248 @@
+// gfx950 kernels of the block-hash path.
+//
+//   k_uniform_glds   : the hot path.  nwaves x 64 equal blocks of bs bytes
+//                      (bs % 128 == 0, 16-byte aligned), one block chain per
+//                      lane, message lines streamed HBM -> LDS by LDS-DMA
+//                      (global_load_lds_dwordx4) in full 128-byte lines.
+//   k_uniform_direct : same contract, each lane loads its own line straight
+//                      into VGPRs one line ahead (A/B variant of the loader).
+//   k_general        : ragged / misaligned blocks, chunk or descriptor form.
+//   k_fill_splitmix64: synthetic test data (bench / tests only).
+//
+// Reference semantics: Hashes::hash_file's per-block split (dir-signature
+// 0.2.9, reached from src/blocks.rs:193 and src/client/sync/uploads.rs:56)
+// and BlockHash::hash_bytes (src/block_id.rs:37-43).
+#include "kernels.hpp"
+
+#include "blake2b_dev.hpp"
+
+namespace cir {
+namespace dev {
+
+// ---------------------------------------------------------------------------
+// LDS image of one wave's message lines (8 KiB, no padding).
+// DMA instruction j (0..7) fills bytes [1024 j, 1024 j + 1024): lane l
+// fetches 16 bytes of block 8j + (l >> 3), chunk (l & 7) ^ (l >> 3) ^ j.
+// So chunk c of wave-block b = 8j + r lives at 1024 j + 128 r + 16 (c^r^j)
+// = 128 b + 16 (c ^ s_b) with s_b = (b ^ (b >> 3)) & 7.
+//   * every DMA instruction reads 8 whole 128-byte lines (coalesced);
+//   * ds_read_b128 of chunk c by lanes b = 0..63 hits 16 distinct bank quads
+//     in every 16-lane group of the b128 read (checked in DESIGN.md), so the
+//     transpose back to one-line-per-lane is conflict free.
+// ---------------------------------------------------------------------------
+constexpr int kWaveLds = 8192;
+constexpr int kWaves = kThreads / 64;
+
+// One wave hashes the 64 equal blocks starting at wsrc (bs bytes each,
+// `lines` = bs / 128 message lines) into out[0 .. 64*32).
+__device__ __forceinline__ void uniform_glds_wave(const uint8_t* __restrict__ wsrc, uint64_t bs,
+                                                  uint32_t lines, uint8_t* __restrict__ out,
+                                                  uint8_t* wl) {
+  const uint32_t lane = threadIdx.x & 63u;
+  // DMA source: uniform line base (+ 8j*bs) + lane offset (r*bs + 16 chunk).
+  const uint32_t r = lane >> 3;
+  const uint32_t dma_lane = (uint32_t)(r * bs) + 16u * ((lane & 7u) ^ r);
+  // LDS read address of chunk c: rd_base ^ 16c.
+  const uint32_t s = (lane ^ (lane >> 3)) & 7u;
+  const uint32_t rd_base = lane * 128u + 16u * s;
+
+  auto issue = [&](uint32_t i) {
+    const uint8_t* line = wsrc + (uint64_t)i * 128u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint8_t* src = line + (uint64_t)j * 8u * bs + (dma_lane ^ (16u * j));
+      __builtin_amdgcn_global_load_lds(
+          (const void __attribute__((address_space(1)))*)src,
+          (void __attribute__((address_space(3)))*)(wl + j * 1024), 16, 0, 0);
+    }
+  };
+
+  uint64_t h[8];
+  init_state(h);
+  uint64_t m[16];
+  issue(0);
+  for (uint32_t i = 0; i < lines; ++i) {
+    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): line i landed in LDS
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const uint4 x = *reinterpret_cast<const uint4*>(wl + (rd_base ^ (16u * c)));
+      m[2 * c] = mk64(x.x, x.y);
+      m[2 * c + 1] = mk64(x.z, x.w);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): reads done before the refill
+    if (i + 1 < lines) issue(i + 1);
+    const bool last = i + 1 == lines;
+    compress(h, m, (uint64_t)(i + 1) * 128u, last);
+  }
+  store_digest(out + lane * 32u, h);
+}
+
+// Pure uniform launch: nblk = gridDim.x * 256 equal blocks.
+__global__ __launch_bounds__(kThreads, 4) void k_uniform_glds(const uint8_t* __restrict__ data,
+                                                               uint64_t bs, uint32_t lines,
+                                                               uint8_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kWaves * kWaveLds];
+  const uint32_t wave = threadIdx.x >> 6;
+  const uint64_t blk0 = ((uint64_t)blockIdx.x * kWaves + wave) * 64u;
+  uniform_glds_wave(data + blk0 * bs, bs, lines, out + blk0 * 32u, lds + wave * kWaveLds);
+}
+
+// Hashes::hash_file over one device-resident file, fused in one launch:
+// workgroups [0, ngen_wg) hash the blocks nuni .. nblk-1 (the ragged rest:
+// fewer than 256 whole blocks plus the short last block) with the general
+// loader, the others hash blocks [0, nuni) 64 per wave through LDS.  The
+// ragged workgroups come first so their chains start with the rest instead
+// of trailing the launch.
+__global__ __launch_bounds__(kThreads, 4) void k_chunks(const uint8_t* __restrict__ data,
+                                                         uint64_t nbytes, uint64_t bs,
+                                                         uint32_t lines, uint64_t nuni,
+                                                         uint64_t nblk, uint32_t ngen_wg,
+                                                         uint8_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kWaves * kWaveLds];
+  if (blockIdx.x < ngen_wg) {
+    const uint64_t b = nuni + (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (b >= nblk) return;
+    const uint64_t o = b * bs, rest = nbytes - o;
+    uint64_t h[8];
+    hash_chain(data + o, rest < bs ? rest : bs, h);
+    store_digest(out + b * 32u, h);
+    return;
+  }
+  const uint32_t wave = threadIdx.x >> 6;
+  const uint64_t blk0 = ((uint64_t)(blockIdx.x - ngen_wg) * kWaves + wave) * 64u;
+  uniform_glds_wave(data + blk0 * bs, bs, lines, out + blk0 * 32u, lds + wave * kWaveLds);
+}
+
+__global__ __launch_bounds__(kThreads, 4) void k_uniform_direct(const uint8_t* __restrict__ data,
+                                                                 uint64_t bs, uint32_t lines,
+                                                                 uint8_t* __restrict__ out) {
+  const uint64_t b = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+  const uint8_t* p = data + b * bs;
+  uint64_t h[8];
+  init_state(h);
+  uint64_t ma[16], mb[16];
+  load_line16(ma, p);
+  for (uint32_t i = 0; i < lines; i += 2) {
+    if (i + 1 < lines) load_line16(mb, p + (uint64_t)(i + 1) * 128u);
+    compress(h, ma, (uint64_t)(i + 1) * 128u, i + 1 == lines);
+    if (i + 1 >= lines) break;
+    if (i + 2 < lines) load_line16(ma, p + (uint64_t)(i + 2) * 128u);
+    compress(h, mb, (uint64_t)(i + 2) * 128u, i + 2 == lines);
+  }
+  store_digest(out + b * 32u, h);
+}
+
+// Chunk form (off == nullptr): block b = [b*bs, min((b+1)*bs, nbytes)) of
+// data, b = first + j.  Descriptor form: block b = (off[b], len[b]) of data,
+// b = perm ? perm[j] : j.
+__global__ __launch_bounds__(kThreads, 4) void k_general(const uint8_t* __restrict__ data,
+                                                          uint64_t nbytes, uint64_t bs,
+                                                          uint64_t first,
+                                                          const uint64_t* __restrict__ off,
+                                                          const uint32_t* __restrict__ len,
+                                                          const uint32_t* __restrict__ perm,
+                                                          uint64_t n, uint8_t* __restrict__ out) {
+  const uint64_t j = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (j >= n) return;
+  uint64_t b, o, l;
+  if (off == nullptr) {
+    b = first + j;
+    o = b * bs;
+    const uint64_t rest = nbytes - o;
+    l = rest < bs ? rest : bs;
+  } else {
+    b = perm ? perm[j] : j;
+    o = off[b];
+    l = len[b];
+  }
+  uint64_t h[8];
+  hash_chain(data + o, l, h);
+  store_digest(out + b * 32u, h);
+}
+
+__device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t k) {
+  uint64_t z = seed + (k + 1) * 0x9e3779b97f4a7c15ULL;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+
+// Word k of the buffer.  block_words == 0: one splitmix64 stream over the
+// whole buffer (word k = output k of splitmix64(seed)).  Otherwise every
+// block of block_words words has its own stream seeded with
+// seed ^ (first_block + block index)  (SURVEY.md 8d config 4).
+__global__ void k_fill_splitmix64(uint64_t* __restrict__ p, uint64_t nwords, uint64_t seed,
+                                  uint64_t block_words, uint64_t first_block) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nwords; k += stride) {
+    uint64_t sd = seed, i = k;
+    if (block_words) {
+      sd = seed ^ (first_block + k / block_words);
+      i = k % block_words;
+    }
+    p[k] = splitmix64_at(sd, i);
+  }
+}
+
+static inline unsigned grid_for(uint64_t n, uint64_t per) { return (unsigned)((n + per - 1) / per); }
+
+hipError_t launch_uniform(Loader loader, const uint8_t* data, uint64_t bs, uint64_t nblk,
+                          uint8_t* out, hipStream_t s) {
+  if (nblk == 0) return hipSuccess;
+  if (nblk % kThreads != 0 || bs % 128u != 0 || bs == 0) return hipErrorInvalidValue;
+  const uint32_t lines = (uint32_t)(bs / 128u);
+  if (loader == Loader::kGlds) {
+    hipLaunchKernelGGL(k_uniform_glds, dim3(grid_for(nblk, kThreads)), dim3(kThreads), 0, s, data,
+                       bs, lines, out);
+  } else {
+    hipLaunchKernelGGL(k_uniform_direct, dim3(grid_for(nblk, kThreads)), dim3(kThreads), 0, s,
+                       data, bs, lines, out);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint8_t* out,
+                         hipStream_t s) {
+  if (nbytes == 0) return hipSuccess;
+  if (bs == 0) return hipErrorInvalidValue;
+  const uint64_t nblk = (nbytes + bs - 1) / bs;
+  const bool uni_ok = bs % 128u == 0 && (reinterpret_cast<uintptr_t>(data) & 15u) == 0 &&
+                      bs / 128u <= 0xffffffffull && bs <= 0xffffffffull / 8u;
+  const uint64_t nuni = uni_ok ? (nbytes / bs) / kThreads * kThreads : 0;
+  const uint64_t ngen_wg = grid_for(nblk - nuni, kThreads);
+  const uint64_t grid = ngen_wg + nuni / kThreads;
+  if (grid > 0x7fffffffull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_chunks, dim3((unsigned)grid), dim3(kThreads), 0, s, data, nbytes, bs,
+                     (uint32_t)(bs / 128u), nuni, nblk, (uint32_t)ngen_wg, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_general_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs,
+                                 uint64_t first, uint64_t n, uint8_t* out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_general, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, data, nbytes,
+                     bs, first, (const uint64_t*)nullptr, (const uint32_t*)nullptr,
+                     (const uint32_t*)nullptr, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_general_desc(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
+                               const uint32_t* perm, uint64_t n, uint8_t* out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_general, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, arena,
+                     (uint64_t)0, (uint64_t)0, (uint64_t)0, off, len, perm, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_splitmix64(uint64_t* p, uint64_t nwords, uint64_t seed,
+                                  uint64_t block_words, uint64_t first_block, hipStream_t s) {
+  if (nwords == 0) return hipSuccess;
+  uint64_t grid = (nwords + 255) / 256;
+  if (grid > 65536) grid = 65536;
+  hipLaunchKernelGGL(k_fill_splitmix64, dim3((unsigned)grid), dim3(256), 0, s, p, nwords, seed,
+                     block_words, first_block);
+  return hipGetLastError();
+}
+
+}  // namespace dev
+}  // namespace cir

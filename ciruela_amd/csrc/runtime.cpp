@@ -1,0 +1,460 @@
+// C ABI of the block-hash path: context, device-resident entry points and the
+// host-memory entry points (pinned double-buffered staging, one worker thread
+// per device).  See include/ciruela_blockhash.h for the reference interface
+// each entry point replaces.
+#include "runtime.hpp"
+
+#include <errno.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdlib>
+#include <thread>
+
+namespace cir {
+
+static thread_local std::string t_last_error;
+
+int fail(int code, const std::string& msg) {
+  t_last_error = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(e == hipErrorOutOfMemory ? CIR_ENOMEM : CIR_EHIP,
+              std::string(what) + ": " + hipGetErrorString(e));
+}
+
+Device::~Device() {
+  (void)hipSetDevice(id);
+  for (Slot& s : slot) {
+    if (s.done) (void)hipEventSynchronize(s.done);
+    (void)hipHostFree(s.h_data);
+    (void)hipHostFree(s.h_off);
+    (void)hipHostFree(s.h_len);
+    (void)hipHostFree(s.h_out);
+    (void)hipFree(s.d_data);
+    (void)hipFree(s.d_off);
+    (void)hipFree(s.d_len);
+    (void)hipFree(s.d_out);
+    if (s.copied) (void)hipEventDestroy(s.copied);
+    if (s.done) (void)hipEventDestroy(s.done);
+  }
+  if (compute) (void)hipStreamDestroy(compute);
+  if (copy) (void)hipStreamDestroy(copy);
+}
+
+int Device::ensure_slot(Slot& s, uint64_t bytes, uint64_t nblk) {
+  if (!s.copied) {
+    CIR_HIP(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
+    CIR_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+  }
+  if (bytes > s.cap) {
+    (void)hipHostFree(s.h_data);
+    (void)hipFree(s.d_data);
+    s.h_data = nullptr;
+    s.d_data = nullptr;
+    s.cap = 0;
+    CIR_HIP(hipHostMalloc(&s.h_data, bytes, hipHostMallocDefault));
+    CIR_HIP(hipMalloc(&s.d_data, bytes));
+    s.cap = bytes;
+  }
+  if (nblk > s.cap_blk) {
+    (void)hipHostFree(s.h_off);
+    (void)hipHostFree(s.h_len);
+    (void)hipHostFree(s.h_out);
+    (void)hipFree(s.d_off);
+    (void)hipFree(s.d_len);
+    (void)hipFree(s.d_out);
+    s.h_off = nullptr;
+    s.h_len = nullptr;
+    s.h_out = nullptr;
+    s.d_off = nullptr;
+    s.d_len = nullptr;
+    s.d_out = nullptr;
+    s.cap_blk = 0;
+    CIR_HIP(hipHostMalloc(&s.h_off, nblk * 8, hipHostMallocDefault));
+    CIR_HIP(hipHostMalloc(&s.h_len, nblk * 4, hipHostMallocDefault));
+    CIR_HIP(hipHostMalloc(&s.h_out, nblk * 32, hipHostMallocDefault));
+    CIR_HIP(hipMalloc(&s.d_off, nblk * 8));
+    CIR_HIP(hipMalloc(&s.d_len, nblk * 4));
+    CIR_HIP(hipMalloc(&s.d_out, nblk * 32));
+    s.cap_blk = nblk;
+  }
+  return CIR_OK;
+}
+
+// Upload a packed slot and hash it.  chunk_bs == 0: descriptor batch
+// (h_off/h_len, nblk blocks); otherwise the slot holds `bytes` consecutive
+// bytes of one file split into chunk_bs blocks (nblk = ceil(bytes / bs)).
+static int slot_submit_impl(Device& d, Slot& s, uint64_t bytes, uint64_t nblk,
+                            uint64_t chunk_bs) {
+  CIR_HIP(hipMemcpyAsync(s.d_data, s.h_data, bytes, hipMemcpyHostToDevice, d.copy));
+  if (chunk_bs == 0) {
+    CIR_HIP(hipMemcpyAsync(s.d_off, s.h_off, nblk * 8, hipMemcpyHostToDevice, d.copy));
+    CIR_HIP(hipMemcpyAsync(s.d_len, s.h_len, nblk * 4, hipMemcpyHostToDevice, d.copy));
+  }
+  CIR_HIP(hipEventRecord(s.copied, d.copy));
+  CIR_HIP(hipStreamWaitEvent(d.compute, s.copied, 0));
+  if (chunk_bs == 0)
+    CIR_HIP(dev::launch_general_desc(s.d_data, s.d_off, s.d_len, nullptr, nblk, s.d_out,
+                                     d.compute));
+  else
+    CIR_HIP(dev::launch_chunks(s.d_data, bytes, chunk_bs, s.d_out, d.compute));
+  CIR_HIP(hipMemcpyAsync(s.h_out, s.d_out, nblk * 32, hipMemcpyDeviceToHost, d.compute));
+  CIR_HIP(hipEventRecord(s.done, d.compute));
+  s.busy = true;
+  return CIR_OK;
+}
+
+int slot_submit(Device& d, Slot& s, uint64_t bytes, uint64_t nblk) {
+  return slot_submit_impl(d, s, bytes, nblk, 0);
+}
+
+int slot_wait(Device& d, Slot& s) {
+  (void)d;
+  if (!s.busy) return CIR_OK;
+  s.busy = false;
+  CIR_HIP(hipEventSynchronize(s.done));
+  return CIR_OK;
+}
+
+static int check_device(int id) {
+  hipDeviceProp_t prop;
+  CIR_HIP(hipGetDeviceProperties(&prop, id));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(CIR_ENODEV, std::string("device ") + std::to_string(id) + " is " +
+                                prop.gcnArchName + ", this build targets gfx950 only");
+  return CIR_OK;
+}
+
+// ---- host-memory batch: cir_hash_blocks --------------------------------
+
+// Hash blocks [b0, b1) of a host arena on device d, packing them 16-byte
+// aligned into the two staging slots (pack slot k+1 while slot k hashes).
+static int run_blocks(cir_ctx* ctx, Device& d, const uint8_t* arena, const uint64_t* off,
+                      const uint32_t* len, size_t b0, size_t b1, uint8_t* out) {
+  std::lock_guard<std::mutex> lk(d.mu);
+  CIR_HIP(hipSetDevice(d.id));
+  const uint64_t cap = ctx->staging;
+  const uint64_t cap_blk = std::max<uint64_t>(cap / 512, 4096);
+  size_t next = b0;
+  size_t pending_first[2] = {0, 0}, pending_n[2] = {0, 0};
+  int k = 0;
+  while (next < b1 || d.slot[0].busy || d.slot[1].busy) {
+    Slot& s = d.slot[k];
+    if (s.busy) {
+      int rc = slot_wait(d, s);
+      if (rc) return rc;
+      memcpy(out + 32 * pending_first[k], s.h_out, 32 * pending_n[k]);
+    }
+    if (next < b1) {
+      // size this batch
+      uint64_t bytes = 0;
+      size_t n = 0;
+      while (next + n < b1 && n < cap_blk) {
+        const uint64_t need = ((bytes + 15) & ~15ull) + len[next + n];
+        if (n > 0 && need > cap) break;
+        bytes = need;
+        ++n;
+      }
+      int rc = d.ensure_slot(s, std::max<uint64_t>(std::max<uint64_t>(bytes, cap), 16),
+                             std::max<uint64_t>(n, cap_blk));
+      if (rc) return rc;
+      uint64_t pos = 0;
+      for (size_t i = 0; i < n; ++i) {
+        pos = (pos + 15) & ~15ull;
+        s.h_off[i] = pos;
+        s.h_len[i] = len[next + i];
+        memcpy(s.h_data + pos, arena + off[next + i], len[next + i]);
+        pos += len[next + i];
+      }
+      rc = slot_submit(d, s, std::max<uint64_t>(pos, 1), n);
+      if (rc) return rc;
+      pending_first[k] = next;
+      pending_n[k] = n;
+      next += n;
+    }
+    k ^= 1;
+  }
+  return CIR_OK;
+}
+
+// Run fn(device, part) on every device of ctx in its own thread; return the
+// first failure.
+static int for_each_device(cir_ctx* ctx, const std::function<int(cir::Device&, size_t)>& fn) {
+  const size_t nd = ctx->devs.size();
+  if (nd == 1) return fn(*ctx->devs[0], 0);
+  std::vector<int> rc(nd, 0);
+  std::vector<std::string> err(nd);
+  std::vector<std::thread> th;
+  for (size_t i = 0; i < nd; ++i)
+    th.emplace_back([&, i] {
+      rc[i] = fn(*ctx->devs[i], i);
+      if (rc[i]) err[i] = t_last_error;
+    });
+  for (auto& t : th) t.join();
+  for (size_t i = 0; i < nd; ++i)
+    if (rc[i]) return fail(rc[i], err[i]);
+  return CIR_OK;
+}
+
+// ---- Hashes::hash_file over a byte source ------------------------------
+
+// read(dst, n) must fill exactly n bytes or return < 0 (errno-style) / the
+// short count at EOF.
+using Reader = std::function<int64_t(uint8_t*, uint64_t)>;
+
+static int run_file(cir_ctx* ctx, const Reader& rd, uint64_t bs, uint64_t* size_out,
+                    std::vector<uint8_t>& hashes) {
+  Device& d = *ctx->devs[0];
+  std::lock_guard<std::mutex> lk(d.mu);
+  CIR_HIP(hipSetDevice(d.id));
+  uint64_t chunk = ctx->staging / bs * bs;
+  if (chunk == 0) chunk = bs;
+  const uint64_t chunk_blk = chunk / bs;
+  uint64_t total = 0;
+  bool eof = false;
+  size_t pending_at[2] = {0, 0}, pending_n[2] = {0, 0};
+  int k = 0;
+  hashes.clear();
+  while (!eof || d.slot[0].busy || d.slot[1].busy) {
+    Slot& s = d.slot[k];
+    if (s.busy) {
+      int rc = slot_wait(d, s);
+      if (rc) return rc;
+      memcpy(hashes.data() + 32 * pending_at[k], s.h_out, 32 * pending_n[k]);
+    }
+    if (!eof) {
+      int rc = d.ensure_slot(s, chunk, chunk_blk);
+      if (rc) return rc;
+      uint64_t got = 0;
+      while (got < chunk) {
+        const int64_t r = rd(s.h_data + got, chunk - got);
+        if (r < 0) return fail(CIR_EIO, std::string("read: ") + strerror((int)-r));
+        if (r == 0) {
+          eof = true;
+          break;
+        }
+        got += (uint64_t)r;
+      }
+      if (got > 0) {
+        const uint64_t n = (got + bs - 1) / bs;
+        pending_at[k] = hashes.size() / 32;
+        pending_n[k] = n;
+        hashes.resize(hashes.size() + 32 * n);
+        rc = slot_submit_impl(d, s, got, n, bs);
+        if (rc) return rc;
+        total += got;
+      }
+    }
+    k ^= 1;
+  }
+  *size_out = total;
+  return CIR_OK;
+}
+
+static int export_hashes(const std::vector<uint8_t>& h, uint8_t** out, size_t* n) {
+  *n = h.size() / 32;
+  *out = nullptr;
+  if (h.empty()) return CIR_OK;
+  *out = (uint8_t*)malloc(h.size());
+  if (!*out) return fail(CIR_ENOMEM, "malloc");
+  memcpy(*out, h.data(), h.size());
+  return CIR_OK;
+}
+
+// Process-default context for cir_blake2b256 (BlockHash::hash_bytes has no
+// context argument in the reference).
+static std::once_flag g_default_once;
+static cir_ctx* g_default = nullptr;
+static int g_default_rc = 0;
+static std::string g_default_err;
+
+static int default_ctx(cir_ctx** out) {
+  std::call_once(g_default_once, [] {
+    g_default_rc = cir_init(&g_default, 1u, 16u << 20);
+    if (g_default_rc) g_default_err = t_last_error;
+  });
+  if (g_default_rc) return fail(g_default_rc, g_default_err);
+  *out = g_default;
+  return CIR_OK;
+}
+
+}  // namespace cir
+
+using namespace cir;
+
+extern "C" {
+
+int cir_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int cir_init(cir_ctx** out, uint32_t device_mask, uint64_t staging_bytes) {
+  if (!out) return fail(CIR_EINVAL, "cir_init: null ctx");
+  *out = nullptr;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0)
+    return fail(CIR_ENODEV, std::string("no HIP device: ") + hipGetErrorString(e));
+  auto ctx = std::make_unique<cir_ctx>();
+  ctx->staging = staging_bytes ? staging_bytes : (256ull << 20);
+  for (int i = 0; i < n && i < 32; ++i) {
+    if (device_mask && !(device_mask & (1u << i))) continue;
+    int rc = check_device(i);
+    if (rc) return rc;
+    auto d = std::make_unique<Device>();
+    d->id = i;
+    CIR_HIP(hipSetDevice(i));
+    CIR_HIP(hipStreamCreateWithFlags(&d->compute, hipStreamNonBlocking));
+    CIR_HIP(hipStreamCreateWithFlags(&d->copy, hipStreamNonBlocking));
+    ctx->devs.push_back(std::move(d));
+  }
+  if (ctx->devs.empty()) return fail(CIR_ENODEV, "device_mask selects no visible device");
+  *out = ctx.release();
+  return CIR_OK;
+}
+
+void cir_destroy(cir_ctx* ctx) { delete ctx; }
+
+int cir_ctx_devices(const cir_ctx* ctx, int* ids, int max_ids) {
+  if (!ctx) return fail(CIR_EINVAL, "null ctx");
+  int n = (int)ctx->devs.size();
+  for (int i = 0; i < n && i < max_ids; ++i) ids[i] = ctx->devs[i]->id;
+  return n;
+}
+
+const char* cir_strerror(int status) {
+  switch (status) {
+    case CIR_OK: return "ok";
+    case CIR_EIO: return "i/o error";
+    case CIR_EINVAL: return "invalid argument";
+    case CIR_EHIP: return "HIP runtime error";
+    case CIR_ENOMEM: return "out of memory";
+    case CIR_EPARSE: return "error parsing index";
+    case CIR_ENOTFOUND: return "not found";
+    case CIR_EHASHSIZE: return "hash size is unsupported";
+    case CIR_ENODEV: return "no usable gfx950 device";
+    case CIR_EUNSUPPORTED: return "unsupported hash type";
+    default: return "unknown error";
+  }
+}
+
+const char* cir_last_error(void) { return t_last_error.c_str(); }
+
+void cir_free(void* p) { free(p); }
+
+int cir_hash_chunks_dev(cir_ctx* ctx, const void* d_data, uint64_t nbytes, uint64_t block_size,
+                        uint8_t* d_out, void* stream) {
+  (void)ctx;
+  if (block_size == 0) return fail(CIR_EINVAL, "block_size must be > 0");
+  if (nbytes && (!d_data || !d_out)) return fail(CIR_EINVAL, "null device pointer");
+  CIR_HIP(dev::launch_chunks((const uint8_t*)d_data, nbytes, block_size, d_out,
+                             (hipStream_t)stream));
+  return CIR_OK;
+}
+
+int cir_hash_blocks_dev(cir_ctx* ctx, const void* d_arena, const uint64_t* d_off,
+                        const uint32_t* d_len, size_t nblk, uint8_t* d_out, void* stream) {
+  (void)ctx;
+  if (nblk && (!d_arena || !d_off || !d_len || !d_out))
+    return fail(CIR_EINVAL, "null device pointer");
+  CIR_HIP(dev::launch_general_desc((const uint8_t*)d_arena, d_off, d_len, nullptr, nblk, d_out,
+                                   (hipStream_t)stream));
+  return CIR_OK;
+}
+
+int cir_hash_blocks(cir_ctx* ctx, const uint8_t* h_arena, const uint64_t* off,
+                    const uint32_t* len, size_t nblk, uint8_t* h_out) {
+  if (!ctx) return fail(CIR_EINVAL, "null ctx");
+  if (nblk == 0) return CIR_OK;
+  if (!h_arena || !off || !len || !h_out) return fail(CIR_EINVAL, "null pointer");
+  // contiguous ranges balanced by bytes
+  const size_t nd = std::min(ctx->devs.size(), nblk);
+  uint64_t total = 0;
+  for (size_t i = 0; i < nblk; ++i) total += len[i] + 128;
+  std::vector<size_t> cut(nd + 1, nblk);
+  cut[0] = 0;
+  uint64_t acc = 0;
+  size_t p = 1;
+  for (size_t i = 0; i < nblk && p < nd; ++i) {
+    acc += len[i] + 128;
+    if (acc * nd >= total * p) cut[p++] = i + 1;
+  }
+  return for_each_device(ctx, [&](Device& d, size_t i) {
+    if (i >= nd || cut[i] >= cut[i + 1]) return (int)CIR_OK;
+    return run_blocks(ctx, d, h_arena, off, len, cut[i], cut[i + 1], h_out);
+  });
+}
+
+int cir_blake2b256(const uint8_t* p, size_t n, uint8_t out[CIR_DIGEST_BYTES]) {
+  if (!out || (n && !p)) return fail(CIR_EINVAL, "null pointer");
+  if (n > 0xffffffffull) return fail(CIR_EINVAL, "block longer than 4 GiB");
+  cir_ctx* ctx = nullptr;
+  int rc = default_ctx(&ctx);
+  if (rc) return rc;
+  static const uint8_t empty = 0;
+  const uint64_t off = 0;
+  const uint32_t len = (uint32_t)n;
+  return cir_hash_blocks(ctx, n ? p : &empty, &off, &len, 1, out);
+}
+
+int cir_hash_file(cir_ctx* ctx, int fd, uint64_t block_size, uint64_t* size_out,
+                  uint8_t** hashes_out, size_t* nhash_out) {
+  if (!ctx || !size_out || !hashes_out || !nhash_out) return fail(CIR_EINVAL, "null pointer");
+  if (block_size == 0) return fail(CIR_EINVAL, "block_size must be > 0");
+  std::vector<uint8_t> h;
+  Reader rd = [fd](uint8_t* dst, uint64_t n) -> int64_t {
+    for (;;) {
+      ssize_t r = ::read(fd, dst, n);
+      if (r < 0 && errno == EINTR) continue;
+      return r < 0 ? -(int64_t)errno : (int64_t)r;
+    }
+  };
+  int rc = run_file(ctx, rd, block_size, size_out, h);
+  if (rc) return rc;
+  return export_hashes(h, hashes_out, nhash_out);
+}
+
+int cir_hash_memory(cir_ctx* ctx, const uint8_t* data, uint64_t size, uint64_t block_size,
+                    uint8_t** hashes_out, size_t* nhash_out) {
+  if (!ctx || !hashes_out || !nhash_out || (size && !data)) return fail(CIR_EINVAL, "null pointer");
+  if (block_size == 0) return fail(CIR_EINVAL, "block_size must be > 0");
+  uint64_t pos = 0, got_size = 0;
+  Reader rd = [&](uint8_t* dst, uint64_t n) -> int64_t {
+    const uint64_t k = std::min(n, size - pos);
+    memcpy(dst, data + pos, k);
+    pos += k;
+    return (int64_t)k;
+  };
+  std::vector<uint8_t> h;
+  int rc = run_file(ctx, rd, block_size, &got_size, h);
+  if (rc) return rc;
+  return export_hashes(h, hashes_out, nhash_out);
+}
+
+int cir_debug_hash_uniform_dev(int loader, const void* d_data, uint64_t block_size, uint64_t nblk,
+                               uint8_t* d_out, void* stream) {
+  if (block_size == 0 || block_size % 128 || nblk % dev::kThreads || (loader != 0 && loader != 1) ||
+      (reinterpret_cast<uintptr_t>(d_data) & 15u))
+    return fail(CIR_EINVAL, "uniform kernel needs bs % 128 == 0, nblk % 256 == 0, 16-B alignment");
+  CIR_HIP(dev::launch_uniform(loader == 0 ? dev::Loader::kGlds : dev::Loader::kDirect,
+                              (const uint8_t*)d_data, block_size, nblk, d_out, (hipStream_t)stream));
+  return CIR_OK;
+}
+
+int cir_fill_splitmix64_dev(void* d_ptr, uint64_t nbytes, uint64_t seed, uint64_t block_bytes,
+                            uint64_t first_block, void* stream) {
+  if (nbytes % 8 || block_bytes % 8) return fail(CIR_EINVAL, "sizes must be multiples of 8");
+  if (nbytes && !d_ptr) return fail(CIR_EINVAL, "null device pointer");
+  CIR_HIP(dev::launch_fill_splitmix64((uint64_t*)d_ptr, nbytes / 8, seed, block_bytes / 8,
+                                      first_block, (hipStream_t)stream));
+  return CIR_OK;
+}
+
+}  // extern "C"

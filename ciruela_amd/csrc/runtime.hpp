@@ -1,0 +1,68 @@
+// Host runtime of the block-hash path: per-device state, error plumbing and
+// the pinned double-buffered staging engine shared by the host-memory entry
+// points (cir_hash_blocks / cir_hash_file / cir_hash_memory / cir_scan_v1).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "ciruela_blockhash.h"
+#include "kernels.hpp"
+
+namespace cir {
+
+int fail(int code, const std::string& msg);
+int hip_fail(hipError_t e, const char* what);
+
+#define CIR_HIP(expr)                                  \
+  do {                                                 \
+    hipError_t cir_e_ = (expr);                        \
+    if (cir_e_ != hipSuccess) return hip_fail(cir_e_, #expr); \
+  } while (0)
+
+// One staging slot: a pinned host buffer and its device twin, plus the
+// descriptor and digest buffers of the blocks packed into it.
+struct Slot {
+  uint8_t* h_data = nullptr;
+  uint8_t* d_data = nullptr;
+  uint64_t cap = 0;
+  uint64_t* h_off = nullptr;
+  uint32_t* h_len = nullptr;
+  uint8_t* h_out = nullptr;
+  uint64_t* d_off = nullptr;
+  uint32_t* d_len = nullptr;
+  uint8_t* d_out = nullptr;
+  uint64_t cap_blk = 0;
+  hipEvent_t copied = nullptr;  // H2D of this slot finished (copy stream)
+  hipEvent_t done = nullptr;    // digests of this slot are back in h_out
+  bool busy = false;
+};
+
+struct Device {
+  int id = 0;
+  hipStream_t compute = nullptr;
+  hipStream_t copy = nullptr;
+  Slot slot[2];
+  std::mutex mu;  // one host-path user at a time per device
+  ~Device();
+  int ensure_slot(Slot& s, uint64_t bytes, uint64_t nblk);
+};
+
+// A batch of blocks already packed in a slot's host buffer:
+// block k = h_data[h_off[k] .. h_off[k] + h_len[k]).
+// Staging engine: the caller packs a slot, submit() uploads and hashes it
+// asynchronously, wait() returns the digests in h_out.
+int slot_submit(Device& d, Slot& s, uint64_t bytes, uint64_t nblk);
+int slot_wait(Device& d, Slot& s);
+
+}  // namespace cir
+
+struct cir_ctx {
+  std::vector<std::unique_ptr<cir::Device>> devs;
+  uint64_t staging = 0;
+};

@@ -1,0 +1,407 @@
+// cir_scan_v1: dir_signature::v1::scan on the GPU path, and index helpers.
+//
+// Reference: the scan call of `ciruela sync` (src/client/sync/uploads.rs:
+// 49-59: ScannerConfig::new, threads(gopt.threads), hash(blake2b_256()),
+// add_dir(dir, "/"), v1::scan(&cfg, &mut index_buf)) and of
+// examples/custom_uploader.rs:59-65.  The crate walks the tree, splits every
+// regular file into block_size blocks and hashes each block on a CPU pool;
+// here host reader threads only stage file bytes into pinned buffers and
+// every block (and the footer) is hashed by the gfx950 kernels.
+//
+// Order of the emitted index (restated from the reference's own re-emitter,
+// MutableIndex::to_raw_data / _emit_dir, src/cluster/download.rs:287-319):
+// a directory line, its files and symlinks sorted by name (bytewise), then
+// its subdirectories recursively in name order.
+#include <dirent.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <map>
+#include <memory>
+#include <thread>
+
+#include "dirsig.hpp"
+#include "runtime.hpp"
+
+namespace cir {
+
+struct ScanFile {
+  std::string real;
+  uint64_t size = 0;
+  uint64_t first_blk = 0;  // global block index of block 0
+};
+
+struct PlanItem {
+  dirsig::EntryKind kind;
+  std::string name;  // kDir: virtual path; else entry name
+  bool exe = false;
+  size_t file = 0;     // kFile: index into files
+  std::string target;  // kLink
+};
+
+static int walk(const std::string& real, const std::string& vpath, std::vector<PlanItem>& plan,
+                std::vector<ScanFile>& files) {
+  DIR* d = opendir(real.c_str());
+  if (!d) return fail(CIR_EIO, "error indexing dir " + real + ": " + strerror(errno));
+  std::vector<std::string> names;
+  while (struct dirent* de = readdir(d)) {
+    if (!strcmp(de->d_name, ".") || !strcmp(de->d_name, "..")) continue;
+    names.emplace_back(de->d_name);
+  }
+  closedir(d);
+  std::sort(names.begin(), names.end());
+  PlanItem di;
+  di.kind = dirsig::EntryKind::kDir;
+  di.name = vpath;
+  plan.push_back(di);
+  std::vector<std::string> subdirs;
+  for (const std::string& n : names) {
+    const std::string p = real + "/" + n;
+    struct stat st;
+    if (lstat(p.c_str(), &st) != 0)
+      return fail(CIR_EIO, "error indexing dir " + p + ": " + strerror(errno));
+    if (S_ISDIR(st.st_mode)) {
+      subdirs.push_back(n);
+    } else if (S_ISREG(st.st_mode)) {
+      PlanItem it;
+      it.kind = dirsig::EntryKind::kFile;
+      it.name = n;
+      it.exe = (st.st_mode & 0111) != 0;
+      it.file = files.size();
+      ScanFile f;
+      f.real = p;
+      f.size = (uint64_t)st.st_size;
+      files.push_back(f);
+      plan.push_back(it);
+    } else if (S_ISLNK(st.st_mode)) {
+      std::string tgt(4096, '\0');
+      const ssize_t r = readlink(p.c_str(), &tgt[0], tgt.size());
+      if (r < 0) return fail(CIR_EIO, "error reading link " + p + ": " + strerror(errno));
+      tgt.resize((size_t)r);
+      PlanItem it;
+      it.kind = dirsig::EntryKind::kLink;
+      it.name = n;
+      it.target = tgt;
+      plan.push_back(it);
+    }
+    // sockets, fifos and devices are not part of an image
+  }
+  for (const std::string& n : subdirs) {
+    const std::string child = vpath == "/" ? "/" + n : vpath + "/" + n;
+    int rc = walk(real + "/" + n, child, plan, files);
+    if (rc) return rc;
+  }
+  return CIR_OK;
+}
+
+struct ReadJob {
+  size_t file;
+  uint64_t file_off;
+  uint64_t len;
+  uint8_t* dst;
+};
+
+static int run_reads(const std::vector<ReadJob>& jobs, const std::vector<ScanFile>& files,
+                     unsigned threads) {
+  std::atomic<size_t> next{0};
+  std::atomic<int> rc{0};
+  std::string err;
+  std::mutex err_mu;
+  auto worker = [&] {
+    for (;;) {
+      const size_t i = next.fetch_add(1);
+      if (i >= jobs.size() || rc.load()) return;
+      const ReadJob& j = jobs[i];
+      const std::string& path = files[j.file].real;
+      const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+      bool ok = fd >= 0;
+      uint64_t got = 0;
+      while (ok && got < j.len) {
+        const ssize_t r = pread(fd, j.dst + got, j.len - got, (off_t)(j.file_off + got));
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) {
+          ok = false;
+          if (r == 0) errno = ENODATA;  // file shrank during the scan
+          break;
+        }
+        got += (uint64_t)r;
+      }
+      const int e = errno;
+      if (fd >= 0) ::close(fd);
+      if (!ok) {
+        std::lock_guard<std::mutex> lk(err_mu);
+        if (!rc.load()) err = "error reading " + path + ": " + strerror(e);
+        rc.store(CIR_EIO);
+        return;
+      }
+    }
+  };
+  const unsigned n = std::max(1u, std::min<unsigned>(threads, (unsigned)jobs.size()));
+  if (n == 1) {
+    worker();
+  } else {
+    std::vector<std::thread> th;
+    for (unsigned i = 0; i < n; ++i) th.emplace_back(worker);
+    for (auto& t : th) t.join();
+  }
+  if (rc.load()) return fail(rc.load(), err);
+  return CIR_OK;
+}
+
+// Hash every block of every file; digests[32*g] for global block g.
+// Batches are packed into the two staging slots of device 0 (file segments
+// 16-byte aligned, one descriptor per block) by `threads` reader threads
+// while the previous batch uploads and hashes.
+static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, unsigned threads,
+                      std::vector<uint8_t>& digests) {
+  uint64_t nblk_total = 0;
+  for (ScanFile& f : files) {
+    f.first_blk = nblk_total;
+    nblk_total += (f.size + bs - 1) / bs;
+  }
+  digests.assign(32 * nblk_total, 0);
+  if (nblk_total == 0) return CIR_OK;
+  Device& d = *ctx->devs[0];
+  std::lock_guard<std::mutex> lk(d.mu);
+  CIR_HIP(hipSetDevice(d.id));
+  const uint64_t cap = std::max<uint64_t>(ctx->staging, bs + 16);
+  const uint64_t cap_blk = std::max<uint64_t>(cap / 512, 4096);
+  size_t fi = 0;       // current file
+  uint64_t fblk = 0;   // next block within it
+  uint64_t pending_first[2] = {0, 0}, pending_n[2] = {0, 0};
+  int k = 0;
+  auto more = [&] {
+    while (fi < files.size() && fblk * bs >= files[fi].size) {
+      ++fi;
+      fblk = 0;
+    }
+    return fi < files.size();
+  };
+  while (more() || d.slot[0].busy || d.slot[1].busy) {
+    Slot& s = d.slot[k];
+    if (s.busy) {
+      int rc = slot_wait(d, s);
+      if (rc) return rc;
+      memcpy(digests.data() + 32 * pending_first[k], s.h_out, 32 * pending_n[k]);
+    }
+    if (more()) {
+      int rc = d.ensure_slot(s, cap, cap_blk);
+      if (rc) return rc;
+      std::vector<ReadJob> jobs;
+      uint64_t pos = 0, n = 0;
+      const uint64_t first = files[fi].first_blk + fblk;
+      while (more() && n < cap_blk) {
+        ScanFile& f = files[fi];
+        const uint64_t left_blk = (f.size + bs - 1) / bs - fblk;
+        pos = (pos + 15) & ~15ull;
+        if (pos + std::min<uint64_t>(bs, f.size - fblk * bs) > cap) break;
+        // as many whole blocks of this file as fit
+        uint64_t take = std::min<uint64_t>(left_blk, cap_blk - n);
+        take = std::min<uint64_t>(take, std::max<uint64_t>((cap - pos) / bs, 1));
+        const uint64_t off0 = fblk * bs;
+        const uint64_t bytes = std::min<uint64_t>(take * bs, f.size - off0);
+        if (pos + bytes > cap) break;
+        for (uint64_t j = 0; j < take; ++j) {
+          s.h_off[n + j] = pos + j * bs;
+          s.h_len[n + j] = (uint32_t)std::min<uint64_t>(bs, f.size - off0 - j * bs);
+        }
+        jobs.push_back({fi, off0, bytes, s.h_data + pos});
+        pos += bytes;
+        n += take;
+        fblk += take;
+      }
+      rc = run_reads(jobs, files, threads);
+      if (rc) return rc;
+      rc = slot_submit(d, s, std::max<uint64_t>(pos, 16), n);
+      if (rc) return rc;
+      pending_first[k] = first;
+      pending_n[k] = n;
+    }
+    k ^= 1;
+  }
+  return CIR_OK;
+}
+
+
+// ---- RawIndex::into_mut + MutableIndex::to_raw_data ---------------------
+// (src/cluster/download.rs:171-188 fill_dirs :108-168, emit :266-319)
+struct TreeItem;
+using Tree = std::map<std::string, TreeItem>;  // BTreeMap<OsString, Item>, bytewise order
+struct TreeItem {
+  dirsig::EntryKind kind = dirsig::EntryKind::kDir;
+  std::unique_ptr<Tree> dir;
+  bool exe = false;
+  uint64_t size = 0;
+  std::vector<uint8_t> hashes;
+  std::string target;
+};
+
+static void split_path(const std::string& p, std::vector<std::string>* parts) {
+  parts->clear();
+  size_t i = 0;
+  while (i < p.size()) {
+    while (i < p.size() && p[i] == '/') ++i;
+    size_t j = i;
+    while (j < p.size() && p[j] != '/') ++j;
+    if (j > i) parts->push_back(p.substr(i, j - i));
+    i = j;
+  }
+}
+
+static void emit_tree(dirsig::Emitter& em, const std::string& path, const Tree& t) {
+  if (t.empty()) return;  // the reference skips empty directories (:292-294)
+  em.start_dir(path);
+  for (const auto& kv : t) {
+    const TreeItem& it = kv.second;
+    if (it.kind == dirsig::EntryKind::kFile)
+      em.add_file(kv.first, it.exe, it.size, it.hashes.data(), it.hashes.size() / 32);
+    else if (it.kind == dirsig::EntryKind::kLink)
+      em.add_symlink(kv.first, it.target);
+  }
+  for (const auto& kv : t)
+    if (kv.second.kind == dirsig::EntryKind::kDir)
+      emit_tree(em, path == "/" ? "/" + kv.first : path + "/" + kv.first, *kv.second.dir);
+}
+
+}  // namespace cir
+
+using namespace cir;
+
+extern "C" {
+
+int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefixes, size_t ndirs,
+                uint64_t block_size, int hash_type, uint32_t threads, uint8_t** index_out,
+                size_t* len_out) {
+  if (!ctx || !index_out || !len_out || (ndirs && !dirs)) return fail(CIR_EINVAL, "null pointer");
+  if (block_size == 0 || block_size > 0xffffffffull)
+    return fail(CIR_EINVAL, "block_size must be in 1 .. 2^32-1");
+  dirsig::Header hdr;
+  hdr.block_size = block_size;
+  if (hash_type == CIR_HASH_BLAKE2B_256)
+    hdr.hash = dirsig::HashType::kBlake2b256;
+  else if (hash_type == CIR_HASH_SHA512_256)
+    return fail(CIR_EUNSUPPORTED, "sha512/256 block hashing is not implemented on the GPU");
+  else
+    return fail(CIR_EINVAL, "unknown hash type");
+  if (threads == 0) threads = std::max(1u, std::thread::hardware_concurrency());
+
+  std::vector<PlanItem> plan;
+  std::vector<ScanFile> files;
+  for (size_t i = 0; i < ndirs; ++i) {
+    std::string pre = prefixes && prefixes[i] ? prefixes[i] : "/";
+    if (pre.empty() || pre[0] != '/') pre = "/" + pre;
+    while (pre.size() > 1 && pre.back() == '/') pre.pop_back();
+    int rc = walk(dirs[i], pre, plan, files);
+    if (rc) return rc;
+  }
+  std::vector<uint8_t> digests;
+  int rc = hash_files(ctx, files, block_size, threads, digests);
+  if (rc) return rc;
+
+  dirsig::Emitter em(hdr);
+  for (const PlanItem& it : plan) {
+    switch (it.kind) {
+      case dirsig::EntryKind::kDir:
+        em.start_dir(it.name);
+        break;
+      case dirsig::EntryKind::kFile: {
+        const ScanFile& f = files[it.file];
+        em.add_file(it.name, it.exe, f.size, digests.data() + 32 * f.first_blk,
+                    (f.size + block_size - 1) / block_size);
+        break;
+      }
+      case dirsig::EntryKind::kLink:
+        em.add_symlink(it.name, it.target);
+        break;
+    }
+  }
+  // Footer = H(every byte after the header line), hashed on the GPU.
+  const std::string& body = em.body();
+  if (body.size() > 0xffffffffull) return fail(CIR_EINVAL, "index body longer than 4 GiB");
+  uint8_t footer[32];
+  const uint64_t off = 0;
+  const uint32_t len = (uint32_t)body.size();
+  static const uint8_t empty = 0;
+  rc = cir_hash_blocks(ctx, body.empty() ? &empty : (const uint8_t*)body.data(), &off, &len, 1,
+                       footer);
+  if (rc) return rc;
+  const std::string out = em.finish(footer, 32);
+  *index_out = (uint8_t*)malloc(out.size());
+  if (!*index_out) return fail(CIR_ENOMEM, "malloc");
+  memcpy(*index_out, out.data(), out.size());
+  *len_out = out.size();
+  return CIR_OK;
+}
+
+// RawIndex::into_mut + MutableIndex::to_raw_data: parse, rebuild the tree and
+// re-emit it in the reference's order with a freshly computed footer.
+int cir_index_rewrite(cir_ctx* ctx, const uint8_t* in, size_t len, uint8_t** out, size_t* out_len) {
+  if (!ctx || !in || !out || !out_len) return fail(CIR_EINVAL, "null pointer");
+  dirsig::Index idx;
+  std::string err;
+  if (!dirsig::parse(in, len, &idx, &err)) return fail(CIR_EPARSE, "ParseError: " + err);
+  if (idx.header.hash != dirsig::HashType::kBlake2b256)
+    return fail(CIR_EUNSUPPORTED, "footer hash sha512/256 is not implemented on the GPU");
+  Tree root;
+  Tree* cur = &root;
+  std::vector<std::string> parts;
+  for (dirsig::Entry& e : idx.entries) {
+    split_path(e.path, &parts);
+    if (e.kind == dirsig::EntryKind::kDir) {
+      cur = &root;
+      for (const std::string& c : parts) {
+        TreeItem& it = (*cur)[c];
+        if (!it.dir) {
+          if (it.kind != dirsig::EntryKind::kDir)
+            return fail(CIR_EPARSE, "The following path conflicts with others: " + e.path);
+          it.dir = std::make_unique<Tree>();
+        }
+        cur = it.dir.get();
+      }
+      continue;
+    }
+    if (parts.empty()) return fail(CIR_EPARSE, "Invalid path in index: " + e.path);
+    TreeItem it;
+    it.kind = e.kind;
+    it.exe = e.exe;
+    it.size = e.size;
+    it.hashes = std::move(e.hashes);
+    it.target = std::move(e.target);
+    (*cur)[parts.back()] = std::move(it);
+  }
+  dirsig::Emitter em(idx.header);
+  emit_tree(em, "/", root);
+  const std::string& body = em.body();
+  if (body.size() > 0xffffffffull) return fail(CIR_EINVAL, "index body longer than 4 GiB");
+  uint8_t footer[32];
+  const uint64_t off = 0;
+  const uint32_t blen = (uint32_t)body.size();
+  static const uint8_t empty = 0;
+  int rc = cir_hash_blocks(ctx, body.empty() ? &empty : (const uint8_t*)body.data(), &off, &blen,
+                           1, footer);
+  if (rc) return rc;
+  const std::string res = em.finish(footer, 32);
+  *out = (uint8_t*)malloc(res.size());
+  if (!*out) return fail(CIR_ENOMEM, "malloc");
+  memcpy(*out, res.data(), res.size());
+  *out_len = res.size();
+  return CIR_OK;
+}
+
+int cir_index_get_hash(const uint8_t* index, size_t len, uint8_t* id_out, size_t* id_len) {
+  if (!index || !id_out || !id_len) return fail(CIR_EINVAL, "null pointer");
+  std::vector<uint8_t> id;
+  std::string err;
+  if (!dirsig::get_hash(index, len, &id, &err)) return fail(CIR_EPARSE, err);
+  if (id.size() > 64) return fail(CIR_EPARSE, "footer longer than 64 bytes");
+  memcpy(id_out, id.data(), id.size());
+  *id_len = id.size();
+  return CIR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,177 @@
+/*
+ * ciruela_blockhash.h — C ABI of the MI355X (gfx950) block-indexing path.
+ *
+ * Drop-in boundary for ciruela's indexing loop.  Every entry
+ * point names the reference interface it replaces (paths are relative to the
+ * tailhook/ciruela v0.6.12 tree).  All hashing runs on the GPU (hand-written
+ * HIP kernels for gfx950); the host side stages bytes and bookkeeps.  There
+ * is no CPU hashing fallback: without a usable GPU every hashing call returns
+ * CIR_ENODEV.
+ *
+ * Conventions
+ *   - return 0 (CIR_OK) on success, a negative CIR_E* code on failure; the
+ *     detail of the last failure is in cir_last_error().  No call aborts the
+ *     process (the reference panics only on impossible states, e.g.
+ *     src/block_id.rs:38,41 "length is ok").
+ *   - digests are 32 raw bytes (BlockHash([u8; 32]), src/block_id.rs:19),
+ *     printed as lowercase hex (src/hexlify.rs:9-13).
+ *   - `stream` arguments are hipStream_t passed as void* (NULL = the null
+ *     stream of the calling thread's current device).  *_dev calls are
+ *     asynchronous on that stream and never synchronise the device.
+ *   - buffers returned through `uint8_t**` are released with cir_free().
+ */
+#ifndef CIRUELA_BLOCKHASH_H
+#define CIRUELA_BLOCKHASH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CIR_DIGEST_BYTES 32
+#define CIR_DEFAULT_BLOCK_SIZE 32768 /* src/daemon/disk/public.rs:154 */
+
+enum cir_status {
+  CIR_OK = 0,
+  CIR_EIO = -1,        /* filesystem error: scan's io::Error (src/client/sync/uploads.rs:57) */
+  CIR_EINVAL = -2,     /* bad argument, length or shape */
+  CIR_EHIP = -3,       /* HIP runtime error (hipError_t text in cir_last_error) */
+  CIR_ENOMEM = -4,     /* host or device allocation failed */
+  CIR_EPARSE = -5,     /* IndexError::ParseError (src/index.rs:64) / DirError::ParseError (src/blocks.rs:117) */
+  CIR_ENOTFOUND = -6,  /* ReadError::NotFound (src/index.rs:78, src/blocks.rs:101) */
+  CIR_EHASHSIZE = -7,  /* DirError::HashSize (src/blocks.rs:123) */
+  CIR_ENODEV = -8,     /* no usable gfx950 device */
+  CIR_EUNSUPPORTED = -9 /* hash type not implemented on the GPU yet */
+};
+
+/* dir-signature HashType (external crate 0.2.9; header tokens in the index) */
+enum cir_hash_type {
+  CIR_HASH_BLAKE2B_256 = 1, /* HashType::blake2b_256()  "blake2b/256" */
+  CIR_HASH_SHA512_256 = 2   /* HashType::sha512_256()   "sha512/256" (parse only) */
+};
+
+typedef struct cir_ctx cir_ctx;
+
+/* ---- context --------------------------------------------------------- */
+
+/* Open the devices in device_mask (bit i = HIP device i; 0 = every visible
+ * device).  staging_bytes (0 = 256 MiB) sizes each device's host->device
+ * staging buffer pair for the host-memory entry points. */
+int cir_init(cir_ctx** ctx, uint32_t device_mask, uint64_t staging_bytes);
+void cir_destroy(cir_ctx* ctx);
+int cir_device_count(void);
+/* devices opened by ctx; ids[i] receives the HIP ordinal of the i-th. */
+int cir_ctx_devices(const cir_ctx* ctx, int* ids, int max_ids);
+const char* cir_strerror(int status);
+const char* cir_last_error(void); /* thread-local detail of the last failure */
+void cir_free(void* p);
+
+/* ---- block hashes ---------------------------------------------------- */
+
+/* BlockHash::hash_bytes(&[u8]) -> BlockHash   (src/block_id.rs:37-43).
+ * Single host buffer, hashed on the process-default device context. */
+int cir_blake2b256(const uint8_t* p, size_t n, uint8_t out[CIR_DIGEST_BYTES]);
+
+/* Device-resident Hashes::hash_file: the bytes [d_data, d_data + nbytes) of
+ * one file already in HBM, split into ceil(nbytes / block_size) blocks (the
+ * last one short; none when nbytes == 0), digest i -> d_out + 32 i.  This is
+ * the metric path (BASELINE.json configs 2 and 4). */
+int cir_hash_chunks_dev(cir_ctx* ctx, const void* d_data, uint64_t nbytes, uint64_t block_size,
+                        uint8_t* d_out, void* stream);
+
+/* Device-resident batch of independent blocks: block b = d_arena[d_off[b] ..
+ * d_off[b] + d_len[b]) -> d_out + 32 b.  Any order, any mix of lengths
+ * (config 3); zero-length blocks hash as the empty input. */
+int cir_hash_blocks_dev(cir_ctx* ctx, const void* d_arena, const uint64_t* d_off,
+                        const uint32_t* d_len, size_t nblk, uint8_t* d_out, void* stream);
+
+/* Host-memory batch (same meaning as cir_hash_blocks_dev, host pointers);
+ * staged through pinned buffers, split across the context's devices. */
+int cir_hash_blocks(cir_ctx* ctx, const uint8_t* h_arena, const uint64_t* off,
+                    const uint32_t* len, size_t nblk, uint8_t* h_out);
+
+/* dir_signature::v1::Hashes::hash_file(HashType::blake2b_256(), block_size,
+ * reader)  (external; call sites src/blocks.rs:193,
+ * src/cluster/download.rs:257).  Reads fd from its current offset to EOF.
+ * *hashes_out = ceil(size / block_size) x 32 bytes (NULL when size == 0). */
+int cir_hash_file(cir_ctx* ctx, int fd, uint64_t block_size, uint64_t* size_out,
+                  uint8_t** hashes_out, size_t* nhash_out);
+
+/* Hashes::hash_file over an in-memory reader (register_memory_blocks,
+ * src/blocks.rs:187-204). */
+int cir_hash_memory(cir_ctx* ctx, const uint8_t* data, uint64_t size, uint64_t block_size,
+                    uint8_t** hashes_out, size_t* nhash_out);
+
+/* ---- index (DIRSIGNATURE.v1) ----------------------------------------- */
+
+/* dir_signature::v1::scan(&ScannerConfig, &mut Vec<u8>)
+ * (src/client/sync/uploads.rs:49-59; examples/custom_uploader.rs:59-65):
+ * ScannerConfig{threads, hash, add_dir(dirs[i], prefixes[i])}.  threads =
+ * host reader threads (gopt.threads, default 4, src/client/global_options.rs:13;
+ * 0 = auto_threads).  *index_out receives the index bytes. */
+int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefixes, size_t ndirs,
+                uint64_t block_size, int hash_type, uint32_t threads, uint8_t** index_out,
+                size_t* len_out);
+
+/* dir_signature::get_hash via InMemoryIndexes::register_index
+ * (src/index.rs:98-105): the image id printed on the index's last line.
+ * id_out must hold 64 bytes; *id_len = decoded length (32 for v1 hashes). */
+int cir_index_get_hash(const uint8_t* index, size_t len, uint8_t* id_out, size_t* id_len);
+
+/* RawIndex::into_mut + MutableIndex::to_raw_data (src/cluster/download.rs:
+ * 171-188, 266-319): parse, rebuild the directory tree and re-emit it in the
+ * reference's order (files and links by name, then subdirectories; empty
+ * directories dropped) with the footer recomputed on the GPU.  blake2b/256
+ * indexes only (CIR_EUNSUPPORTED for sha512/256 until its kernel exists). */
+int cir_index_rewrite(cir_ctx* ctx, const uint8_t* in, size_t len, uint8_t** out, size_t* out_len);
+
+/* ---- consumers of the index (host bookkeeping) ------------------------ */
+
+/* InMemoryIndexes (src/index.rs:53-124): ImageId -> index bytes. */
+typedef struct cir_indexes cir_indexes;
+cir_indexes* cir_indexes_new(void);
+void cir_indexes_free(cir_indexes* h);
+/* register_index (src/index.rs:98-105); id_out holds 64 bytes. */
+int cir_indexes_register(cir_indexes* h, const uint8_t* data, size_t len, uint8_t* id_out,
+                         size_t* id_len);
+/* GetIndex::read_index (src/index.rs:106-123); CIR_ENOTFOUND if absent. */
+int cir_indexes_read(cir_indexes* h, const uint8_t* id, size_t id_len, uint8_t** data_out,
+                     size_t* len_out);
+
+/* ThreadedBlockReader (src/blocks.rs:85-240): BlockHash -> block bytes. */
+typedef struct cir_blocks cir_blocks;
+cir_blocks* cir_blocks_new(void);
+void cir_blocks_free(cir_blocks* h);
+size_t cir_blocks_len(cir_blocks* h);
+/* register_dir (src/blocks.rs:145-183): CIR_EPARSE / CIR_EHASHSIZE. */
+int cir_blocks_register_dir(cir_blocks* h, const char* dir, const uint8_t* index, size_t len);
+/* register_memory_blocks (src/blocks.rs:187-204), hashed on the GPU. */
+int cir_blocks_register_memory(cir_ctx* ctx, cir_blocks* h, const uint8_t* data, size_t len,
+                               uint64_t block_size);
+/* GetBlock::read_block (src/blocks.rs:207-240); CIR_ENOTFOUND if absent. */
+int cir_blocks_read(cir_blocks* h, const uint8_t hash[CIR_DIGEST_BYTES], uint8_t** data_out,
+                    size_t* len_out);
+
+/* ---- test data -------------------------------------------------------- */
+
+/* Fill d_ptr with splitmix64 words (bench/tests only).  block_bytes == 0:
+ * word k = splitmix64 output k of `seed`; otherwise block i (block_bytes
+ * each, a multiple of 8) is its own stream seeded seed ^ (first_block + i). */
+int cir_fill_splitmix64_dev(void* d_ptr, uint64_t nbytes, uint64_t seed, uint64_t block_bytes,
+                            uint64_t first_block, void* stream);
+
+/* ---- diagnostics (not part of the reference interface) ---------------- */
+
+/* One launch of a uniform-block kernel variant, for A/B measurement:
+ * loader 0 = LDS-DMA coalesced lines (the production loader), 1 = per-lane
+ * direct loads.  nblk % 256 == 0, block_size % 128 == 0, d_data 16-B aligned. */
+int cir_debug_hash_uniform_dev(int loader, const void* d_data, uint64_t block_size, uint64_t nblk,
+                               uint8_t* d_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CIRUELA_BLOCKHASH_H */

@@ -1,0 +1,220 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.  Never linked into, loaded by or called
+ * from the product (ciruela_amd/); only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg use it, as the checker / CPU baseline.
+ *
+ * CPU restatement of the reference's block-hash algorithm:
+ *   BlockHash::hash_bytes (reference src/block_id.rs:37-43) =
+ *     blake2 0.7.1 `Blake2b::VariableOutput::new(32)` + input + variable_result
+ *   = BLAKE2b (RFC 7693) with digest length nn = 32, no key, encoded in the
+ *     parameter block (p[0] = 0x01010000 ^ (kk << 8) ^ nn, RFC 7693 2.5/3.3).
+ *   dir-signature 0.2.9 `Hashes::hash_file(hash, block_size, reader)`
+ *   (called at src/blocks.rs:193, src/cluster/download.rs:257) = that hash
+ *   over every block_size chunk of the file, last chunk short, no chunk for an
+ *   empty file (fixture src/cluster/download.rs:361 "test.txt f 0").
+ * The blake2/dir-signature crates are not vendored in the reference and Rust
+ * is not installed, so this is a restatement of RFC 7693 (blake2 0.7.1,
+ * Cargo.lock:110-117, implements RFC 7693); it is pinned by the RFC's
+ * Appendix A vector and by vectors generated with Python hashlib
+ * (tests/golden/make_golden.py), see tests/test_oracle.py.
+ *
+ * Build: oracle/Makefile -> oracle/build/liboracle_blake2b.so
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+static const uint64_t IV[8] = {
+    0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL, 0xa54ff53a5f1d36f1ULL,
+    0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL, 0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+
+/* RFC 7693 section 2.7 */
+static const uint8_t SIGMA[12][16] = {
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+    {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+    {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4},
+    {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+    {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13},
+    {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+    {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11},
+    {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+    {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5},
+    {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+    {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
+
+static inline uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+
+static inline uint64_t load64(const uint8_t* p) {
+  uint64_t v = 0;
+  for (int i = 7; i >= 0; --i) v = (v << 8) | p[i];
+  return v;
+}
+
+/* F (RFC 7693 section 3.2) */
+static void compress(uint64_t h[8], const uint8_t block[128], uint64_t t0, uint64_t t1, int last) {
+  uint64_t v[16], m[16];
+  for (int i = 0; i < 16; ++i) m[i] = load64(block + 8 * i);
+  for (int i = 0; i < 8; ++i) {
+    v[i] = h[i];
+    v[i + 8] = IV[i];
+  }
+  v[12] ^= t0;
+  v[13] ^= t1;
+  if (last) v[14] = ~v[14];
+#define G(a, b, c, d, x, y)          \
+  do {                               \
+    v[a] = v[a] + v[b] + (x);        \
+    v[d] = rotr64(v[d] ^ v[a], 32);  \
+    v[c] = v[c] + v[d];              \
+    v[b] = rotr64(v[b] ^ v[c], 24);  \
+    v[a] = v[a] + v[b] + (y);        \
+    v[d] = rotr64(v[d] ^ v[a], 16);  \
+    v[c] = v[c] + v[d];              \
+    v[b] = rotr64(v[b] ^ v[c], 63);  \
+  } while (0)
+  for (int r = 0; r < 12; ++r) {
+    const uint8_t* s = SIGMA[r];
+    G(0, 4, 8, 12, m[s[0]], m[s[1]]);
+    G(1, 5, 9, 13, m[s[2]], m[s[3]]);
+    G(2, 6, 10, 14, m[s[4]], m[s[5]]);
+    G(3, 7, 11, 15, m[s[6]], m[s[7]]);
+    G(0, 5, 10, 15, m[s[8]], m[s[9]]);
+    G(1, 6, 11, 12, m[s[10]], m[s[11]]);
+    G(2, 7, 8, 13, m[s[12]], m[s[13]]);
+    G(3, 4, 9, 14, m[s[14]], m[s[15]]);
+  }
+#undef G
+  for (int i = 0; i < 8; ++i) h[i] ^= v[i] ^ v[i + 8];
+}
+
+/* BLAKE2b with outlen (1..64) bytes, unkeyed (RFC 7693 section 3.3). */
+int oracle_blake2b(uint8_t* out, size_t outlen, const uint8_t* in, size_t inlen) {
+  if (outlen == 0 || outlen > 64) return -1;
+  uint64_t h[8];
+  memcpy(h, IV, sizeof h);
+  h[0] ^= 0x01010000ULL ^ (uint64_t)outlen;
+  uint64_t t0 = 0, t1 = 0;
+  uint8_t buf[128];
+  /* all but the last block */
+  while (inlen > 128) {
+    t0 += 128;
+    if (t0 < 128) ++t1;
+    compress(h, in, t0, t1, 0);
+    in += 128;
+    inlen -= 128;
+  }
+  /* last block (possibly empty), zero padded */
+  memset(buf, 0, sizeof buf);
+  memcpy(buf, in, inlen);
+  t0 += inlen;
+  if (t0 < inlen) ++t1;
+  compress(h, buf, t0, t1, 1);
+  for (size_t i = 0; i < outlen; ++i) out[i] = (uint8_t)(h[i / 8] >> (8 * (i % 8)));
+  return 0;
+}
+
+/* BlockHash::hash_bytes */
+int oracle_blake2b256(uint8_t out[32], const uint8_t* in, size_t inlen) {
+  return oracle_blake2b(out, 32, in, inlen);
+}
+
+/* ---- batch forms, threaded (CPU baseline: dir-signature hashes on a CPU
+ *      pool of `threads` workers; here the unit of work is a block) ---- */
+
+struct job {
+  const uint8_t* arena;
+  const uint64_t* off;
+  const uint32_t* len;
+  uint64_t nbytes, bs; /* chunk form when off == NULL */
+  uint8_t* out;
+  size_t n;
+  size_t next;
+  pthread_mutex_t mu;
+};
+
+static void* worker(void* arg) {
+  struct job* j = (struct job*)arg;
+  for (;;) {
+    pthread_mutex_lock(&j->mu);
+    size_t b0 = j->next;
+    j->next += 64;
+    pthread_mutex_unlock(&j->mu);
+    if (b0 >= j->n) return NULL;
+    size_t b1 = b0 + 64 < j->n ? b0 + 64 : j->n;
+    for (size_t b = b0; b < b1; ++b) {
+      if (j->off) {
+        oracle_blake2b256(j->out + 32 * b, j->arena + j->off[b], j->len[b]);
+      } else {
+        uint64_t o = (uint64_t)b * j->bs;
+        uint64_t l = j->nbytes - o < j->bs ? j->nbytes - o : j->bs;
+        oracle_blake2b256(j->out + 32 * b, j->arena + o, l);
+      }
+    }
+  }
+}
+
+static int run(struct job* j, int threads) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_mutex_init(&j->mu, NULL);
+  j->next = 0;
+  pthread_t th[256];
+  int started = 0;
+  for (int i = 1; i < threads; ++i)
+    if (pthread_create(&th[started], NULL, worker, j) == 0) ++started;
+  worker(j);
+  for (int i = 0; i < started; ++i) pthread_join(th[i], NULL);
+  pthread_mutex_destroy(&j->mu);
+  return 0;
+}
+
+/* block b = arena[off[b] .. off[b] + len[b]) -> out + 32 b */
+int oracle_hash_blocks(const uint8_t* arena, const uint64_t* off, const uint32_t* len, size_t n,
+                       uint8_t* out, int threads) {
+  struct job j;
+  memset(&j, 0, sizeof j);
+  j.arena = arena;
+  j.off = off;
+  j.len = len;
+  j.out = out;
+  j.n = n;
+  return run(&j, threads);
+}
+
+/* Hashes::hash_file over a memory buffer: ceil(nbytes / bs) digests */
+int oracle_hash_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint8_t* out,
+                       int threads) {
+  if (bs == 0) return -1;
+  struct job j;
+  memset(&j, 0, sizeof j);
+  j.arena = data;
+  j.nbytes = nbytes;
+  j.bs = bs;
+  j.out = out;
+  j.n = (size_t)((nbytes + bs - 1) / bs);
+  return run(&j, threads);
+}
+
+/* Host twin of the product's synthetic-data kernel (k_fill_splitmix64),
+ * used to regenerate sampled blocks for checking. */
+static inline uint64_t splitmix64_at(uint64_t seed, uint64_t k) {
+  uint64_t z = seed + (k + 1) * 0x9e3779b97f4a7c15ULL;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+
+/* Fill words [word0, word0 + nwords) of the synthetic buffer into dst. */
+void oracle_splitmix64_fill(uint64_t* dst, uint64_t word0, uint64_t nwords, uint64_t seed,
+                            uint64_t block_words, uint64_t first_block) {
+  for (uint64_t i = 0; i < nwords; ++i) {
+    uint64_t k = word0 + i, s = seed, w = k;
+    if (block_words) {
+      s = seed ^ (first_block + k / block_words);
+      w = k % block_words;
+    }
+    dst[i] = splitmix64_at(s, w);
+  }
+}

@@ -1,0 +1,125 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY (never imported by ciruela_amd/).
+
+Pure-Python restatement of the parts of dir-signature 0.2.9 (external crate,
+Cargo.toml:35, not vendored in the reference) that ciruela's indexing path
+uses, for small trees:
+
+* `emit(header, tree)` — the DIRSIGNATURE.v1 text as the reference's own
+  re-emitter writes it (MutableIndex::to_raw_data, src/cluster/download.rs:
+  266-319): header line, then per directory a "/path" line, its files and
+  symlinks sorted by name ("  name f|x size hash..." / "  name s target"),
+  then its subdirectories; footer line = hex(H(every byte after the header
+  line)).  Pinned by the reference fixture src/cluster/download.rs:357-366
+  (tests/golden/dirsig_v1_example.json, checked in tests/test_dirsig.py).
+* `scan(path, block_size)` — the v1::scan of `ciruela sync`
+  (src/client/sync/uploads.rs:49-59) with blake2b/256 per-block hashes
+  (BlockHash::hash_bytes, src/block_id.rs:37-43 = RFC 7693 BLAKE2b, nn=32,
+  computed with hashlib, pinned in tests/test_oracle.py).  Unlike the
+  re-emitter, the scanner keeps empty directories (unverified against the
+  crate: DESIGN.md "Index format").
+* escaping of names outside printable ASCII as \\xNN (unverified).
+"""
+import hashlib
+import os
+import stat
+
+
+def h_blake2b256(data):
+    return hashlib.blake2b(data, digest_size=32).digest()
+
+
+def h_sha512_256(data):
+    return hashlib.new("sha512_256", data).digest()
+
+
+HASHES = {"blake2b/256": h_blake2b256, "sha512/256": h_sha512_256}
+
+
+def escape(raw):
+    out = []
+    for c in raw:
+        if c <= 0x20 or c >= 0x7F or c == 0x5C:
+            out.append(b"\\x%02x" % c)
+        else:
+            out.append(bytes([c]))
+    return b"".join(out)
+
+
+def block_hashes(data, block_size, hash_name="blake2b/256"):
+    """Hashes::hash_file: one digest per block_size chunk, none for b''."""
+    h = HASHES[hash_name]
+    return [h(data[i:i + block_size]) for i in range(0, len(data), block_size)]
+
+
+def emit(hash_name, block_size, dirs, keep_empty=False):
+    """dirs: list of (vpath bytes, [entries]) in emission order, entry =
+    ('f', name, exe, size, [digests]) or ('s', name, target)."""
+    header = b"DIRSIGNATURE.v1 %s block_size=%d\n" % (hash_name.encode(), block_size)
+    body = []
+    for vpath, entries in dirs:
+        if not entries and not keep_empty:
+            continue
+        body.append(escape(vpath) + b"\n")
+        for e in entries:
+            if e[0] == "f":
+                _, name, exe, size, digests = e
+                line = b"  " + escape(name) + (b" x " if exe else b" f ") + str(size).encode()
+                for d in digests:
+                    line += b" " + d.hex().encode()
+                body.append(line + b"\n")
+            else:
+                _, name, target = e
+                body.append(b"  " + escape(name) + b" s " + escape(target) + b"\n")
+    body = b"".join(body)
+    footer = HASHES[hash_name](body).hex().encode() + b"\n"
+    return header + body + footer
+
+
+def scan(root, block_size=32768, hash_name="blake2b/256"):
+    """Index bytes of the tree at `root` (mounted at '/')."""
+    dirs = []
+
+    def walk(real, vpath):
+        names = sorted(os.listdir(os.fsencode(real)))
+        entries, subdirs = [], []
+        for n in names:
+            p = os.path.join(os.fsencode(real), n)
+            st = os.lstat(p)
+            if stat.S_ISDIR(st.st_mode):
+                subdirs.append(n)
+            elif stat.S_ISREG(st.st_mode):
+                with open(p, "rb") as f:
+                    data = f.read()
+                entries.append(("f", n, bool(st.st_mode & 0o111), len(data),
+                                block_hashes(data, block_size, hash_name)))
+            elif stat.S_ISLNK(st.st_mode):
+                entries.append(("s", n, os.readlink(p)))
+        dirs.append((vpath, entries))
+        for n in subdirs:
+            walk(os.path.join(os.fsencode(real), n),
+                 (b"/" + n) if vpath == b"/" else vpath + b"/" + n)
+
+    walk(root, b"/")
+    return emit(hash_name, block_size, dirs, keep_empty=True)
+
+
+def parse(index):
+    """(hash_name, block_size, dirs, footer) of an index (test helper)."""
+    lines = index.split(b"\n")
+    assert lines[-1] == b""
+    head = lines[0].split(b" ")
+    assert head[0] == b"DIRSIGNATURE.v1"
+    hash_name = head[1].decode()
+    bs = int(head[2].split(b"=")[1])
+    dirs = []
+    for ln in lines[1:-2]:
+        if ln.startswith(b"/"):
+            dirs.append((ln, []))
+        else:
+            parts = ln[2:].split(b" ")
+            if parts[1] in (b"f", b"x"):
+                dirs[-1][1].append(("f", parts[0], parts[1] == b"x", int(parts[2]),
+                                    [bytes.fromhex(x.decode()) for x in parts[3:]]))
+            else:
+                dirs[-1][1].append(("s", parts[0], parts[2]))
+    return hash_name, bs, dirs, bytes.fromhex(lines[-2].decode())

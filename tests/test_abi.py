@@ -1,0 +1,144 @@
+"""C ABI and host logic without a GPU (CPU-only).
+
+* the library loads and exports every symbol include/*.h declares;
+* error behaviour without a device (no silent CPU fallback);
+* index parsing / ImageId / registries (pure host bookkeeping) against the
+  reference's fixture (src/cluster/download.rs:357-366).
+"""
+import glob
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+import ciruela_amd as ca
+from ciruela_amd import _native
+
+
+def declared_symbols():
+    syms = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        text = open(h).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        for m in re.finditer(r"\b(cir_[a-z0-9_]+)\s*\(", text):
+            syms.add(m.group(1))
+    return syms
+
+
+def test_exports_every_declared_symbol():
+    decl = declared_symbols()
+    assert len(decl) >= 25
+    out = subprocess.check_output(["nm", "-D", "--defined-only", _native.LIB_PATH]).decode()
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    missing = decl - exported
+    assert not missing, missing
+    # and the Python binding covers all of them
+    assert decl <= set(_native.EXPORTED) | {"cir_init"}
+
+
+def test_library_is_gfx950_code():
+    """The embedded fat binary carries gfx950 code objects (and only those)."""
+    blob = open(_native.LIB_PATH, "rb").read()
+    targets = set(re.findall(rb"hipv4-amdgcn-amd-amdhsa--(gfx[0-9a-z]+)", blob))
+    assert targets == {b"gfx950"}, targets
+
+
+def test_strerror_codes():
+    for code in range(-9, 1):
+        assert _native.lib.cir_strerror(code)
+    assert _native.lib.cir_strerror(_native.CIR_ENOTFOUND) == b"not found"
+
+
+def test_no_device_is_loud():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("this container has no GPU; only meaningful without one")
+    with pytest.raises(ca.NoDevice):
+        ca.Context()
+    with pytest.raises(ca.NoDevice):
+        ca.BlockHash.hash_bytes(b"abc")
+
+
+def test_get_hash_and_image_id(dirsig_example):
+    idx = dirsig_example["index"].encode()
+    raw = ca.get_hash(idx)
+    assert raw.hex() == "552ca5730ee95727e890a2155c88609d244624034ff70de264cf88220d11d6df"
+    iid = ca.ImageId(raw)
+    assert str(iid) == raw.hex()
+    assert ca.ImageId.from_str(raw.hex()) == iid
+    with pytest.raises(ca.CiruelaError):
+        ca.get_hash(b"DIRSIGNATURE.v1 blake2b/256 block_size=32768\n/\nnot-hex\n")
+
+
+def test_in_memory_indexes(dirsig_example):
+    idx = dirsig_example["index"].encode()
+    reg = ca.InMemoryIndexes()
+    iid = reg.register_index(idx)
+    assert reg.read_index(iid) == idx
+    with pytest.raises(ca.ReadError) as e:
+        reg.read_index(ca.ImageId(bytes(32)))
+    assert e.value.status == _native.CIR_ENOTFOUND
+    with pytest.raises(ca.IndexError_):
+        reg.register_index(b"garbage")
+
+
+def test_register_dir_and_read_block(tmp_path, dirsig_example):
+    """ThreadedBlockReader::register_dir (src/blocks.rs:145-183) on the
+    reference fixture: one block per non-empty file, Disk{path, 0, size}."""
+    idx = dirsig_example["index"].encode()
+    (tmp_path / "subdir").mkdir()
+    (tmp_path / "subdir" / ".hidden").write_bytes(b"Hidden\n")
+    r = ca.ThreadedBlockReader()
+    r.register_dir(str(tmp_path), idx)
+    assert len(r) == 3  # hello.txt, .hidden, file.txt (test.txt is empty)
+    h = bytes.fromhex("6d7f5f9804ee4dbc1ff7e12c7665387e0119e8ea629996c52d38b75c12ad0acf")
+    assert r.read_block(ca.BlockHash(h)) == b"Hidden\n"
+    with pytest.raises(ca.ReadError):  # hello.txt is not on disk
+        r.read_block(bytes.fromhex(
+            "a79eef66019bfb9a41f798f2cff2d2d36ed294cc3f96bf53bbfc5192ebe60192"))
+    with pytest.raises(ca.ReadError) as e:
+        r.read_block(bytes(32))
+    assert e.value.status == _native.CIR_ENOTFOUND
+
+
+def test_register_dir_multiblock(tmp_path):
+    """Block pointers: offset = idx * bs, size = min(left, bs)."""
+    data = bytes(range(256)) * 40  # 10240 bytes, bs 4096 -> 3 blocks
+    (tmp_path / "f.bin").write_bytes(data)
+    hs = [bytes([i]) * 32 for i in range(3)]
+    idx = (b"DIRSIGNATURE.v1 blake2b/256 block_size=4096\n/\n  f.bin f 10240 " +
+           b" ".join(h.hex().encode() for h in hs) + b"\n" + b"ab" * 32 + b"\n")
+    r = ca.ThreadedBlockReader()
+    r.register_dir(str(tmp_path), idx)
+    assert r.read_block(hs[0]) == data[:4096]
+    assert r.read_block(hs[1]) == data[4096:8192]
+    assert r.read_block(hs[2]) == data[8192:]
+
+
+def test_register_dir_errors(tmp_path):
+    r = ca.ThreadedBlockReader()
+    with pytest.raises(ca.DirError) as e:
+        r.register_dir(str(tmp_path), b"DIRSIGNATURE.v1 blake2b/256 block_size=4096\n/\n"
+                                      b"  f f 10 zz\n" + b"ab" * 32 + b"\n")
+    assert e.value.status == _native.CIR_EPARSE
+    with pytest.raises(ca.DirError):  # wrong number of hashes for the size
+        r.register_dir(str(tmp_path), b"DIRSIGNATURE.v1 blake2b/256 block_size=4096\n/\n"
+                                      b"  f f 5000 " + b"ab" * 32 + b"\n" + b"ab" * 32 + b"\n")
+
+
+def test_block_hash_type():
+    h = ca.BlockHash(bytes(range(32)))
+    assert str(h) == bytes(range(32)).hex()
+    assert repr(h).startswith("BlockHash(")
+    assert ca.BlockHash.from_bytes(b"x" * 31) is None
+    assert ca.BlockHash.from_bytes(b"x" * 32) == ca.BlockHash(b"x" * 32)
+    assert len({ca.BlockHash(b"x" * 32), ca.BlockHash(b"x" * 32)}) == 1
+
+
+def test_cli_usage():
+    cli = os.path.join(ROOT, "bin", "ciruela-index")
+    p = subprocess.run([cli], capture_output=True)
+    assert p.returncode == 2 and b"usage" in p.stderr

@@ -1,0 +1,104 @@
+"""Parity at BASELINE.json's full sizes on one MI355X.
+
+Config 2 (1 M x 32 KiB = 32 GiB) and config 3 (10 GiB of mixed 4 KiB /
+32 KiB / 1 MiB blocks, 10 % ragged, shuffled).  The oracle cannot redo
+32 GiB in seconds, so these check size-independent properties plus a large
+random sample against the oracle:
+  * golden digests of the special config-2 blocks (0-15 zero, 16-31 range);
+  * a seeded random sample of blocks (and the last ones) regenerated on the
+    host and hashed by the oracle;
+  * determinism: a second launch gives the identical digest array, and the
+    per-lane direct loader gives the same array as the LDS-DMA loader.
+"""
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+BS = 32768
+SEED_C2 = 0x5EED0002
+
+
+def host_words(oracle, word0, nwords, seed):
+    buf = np.empty(nwords, dtype=np.uint64)
+    oracle.oracle_splitmix64_fill(buf.ctypes.data, word0, nwords, seed, 0, 0)
+    return buf
+
+
+def test_config2_full(gpu, oracle, vectors):
+    import torch
+    nblk = 1 << 20
+    nbytes = nblk * BS
+    data = torch.empty(nbytes, dtype=torch.uint8, device="cuda:0")
+    gpu._n.check(gpu._n.lib.cir_fill_splitmix64_dev(data.data_ptr(), nbytes, SEED_C2, 0, 0, 0))
+    data[:16 * BS].zero_()
+    data[16 * BS:32 * BS].copy_(torch.arange(256, device="cuda:0").to(torch.uint8).repeat(16 * 128))
+    ctx = gpu.Context(device_mask=1)
+    out = torch.empty(nblk * 32, dtype=torch.uint8, device="cuda:0")
+    ctx.hash_chunks_dev(data.data_ptr(), nbytes, BS, out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().reshape(nblk, 32)
+    gold = vectors["config2"]
+    for i in range(16):
+        assert got[i].tobytes().hex() == gold["zero_block"]
+    for i in range(16, 32):
+        assert got[i].tobytes().hex() == gold["range_block"]
+    rng = random.Random(2)
+    sample = sorted(set(rng.randrange(32, nblk) for _ in range(3000)) | set(range(nblk - 64, nblk)))
+    for b in sample:
+        words = host_words(oracle, b * BS // 8, BS // 8, SEED_C2)
+        want = np.zeros(32, dtype=np.uint8)
+        oracle.oracle_hash_chunks(words.ctypes.data, BS, BS, want.ctypes.data, 1)
+        assert got[b].tobytes() == want.tobytes(), "block %d" % b
+    # determinism + loader A/B at full size
+    out2 = torch.empty_like(out)
+    gpu._n.check(gpu._n.lib.cir_debug_hash_uniform_dev(1, data.data_ptr(), BS, nblk,
+                                                       out2.data_ptr(), 0))
+    ctx.hash_chunks_dev(data.data_ptr(), nbytes, BS, out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    assert torch.equal(out, out2)
+    assert np.array_equal(out.cpu().numpy().reshape(nblk, 32), got)
+    del data
+
+
+def test_config3_full(gpu, oracle):
+    """10 GiB: equal bytes per class, 10% ragged U[1, size-1], shuffled."""
+    import torch
+    total = 10 << 30
+    rng = random.Random(0x5EED0003)
+    lens = []
+    for size in (4096, 32768, 1 << 20):
+        count = (total // 3) // size
+        lens += [rng.randrange(1, size) if rng.random() < 0.1 else size for _ in range(count)]
+    order = list(range(len(lens)))
+    rng.shuffle(order)
+    lens = [lens[i] for i in order]
+    # arena: blocks back to back at 128-B aligned offsets in descriptor order
+    l64 = np.array(lens, dtype=np.uint64)
+    padded = (l64 + 127) // 128 * 128
+    offs = np.zeros(len(lens), dtype=np.uint64)
+    offs[1:] = np.cumsum(padded)[:-1]
+    nbytes = int(offs[-1] + padded[-1])
+    data = torch.empty(nbytes, dtype=torch.uint8, device="cuda:0")
+    seed = 0x5EED0003
+    gpu._n.check(gpu._n.lib.cir_fill_splitmix64_dev(data.data_ptr(), nbytes, seed, 0, 0, 0))
+    d_off = torch.from_numpy(offs.view(np.int64)).to("cuda:0")
+    d_len = torch.from_numpy(np.array(lens, dtype=np.int32)).to("cuda:0")
+    out = torch.empty(32 * len(lens), dtype=torch.uint8, device="cuda:0")
+    ctx = gpu.Context(device_mask=1)
+    ctx.hash_blocks_dev(data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), len(lens),
+                        out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().reshape(-1, 32)
+    idx = rng.sample(range(len(lens)), 2500)
+    idx += [i for i in range(len(lens)) if lens[i] == 1 << 20][:20]
+    for i in idx:
+        o, n = int(offs[i]), lens[i]
+        words = host_words(oracle, o // 8, (n + 7) // 8, seed)
+        want = np.zeros(32, dtype=np.uint8)
+        oracle.oracle_hash_chunks(words.ctypes.data, n, max(n, 1), want.ctypes.data, 1)
+        if n == 0:
+            continue
+        assert got[i].tobytes() == want.tobytes(), "block %d len %d" % (i, n)

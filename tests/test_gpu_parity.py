@@ -1,0 +1,312 @@
+"""GPU parity: every digest from the gfx950 kernels equals the oracle's.
+
+Bit-exact (byte work).  Sizes small enough for the oracle to finish in
+seconds; the full BASELINE sizes are in test_gpu_fullsize.py.  All calls go
+through the C ABI (libciruela_amd.so).
+"""
+import ctypes
+import os
+import random
+
+import numpy as np
+import pytest
+
+from conftest import oracle_digest
+from make_golden import gen_bytes
+
+import dirsig_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx(gpu):
+    return gpu.Context(device_mask=1, staging_bytes=8 << 20)
+
+
+@pytest.fixture(scope="module")
+def small_ctx(gpu):
+    # tiny staging buffers: forces many double-buffered batches
+    return gpu.Context(device_mask=1, staging_bytes=1 << 20)
+
+
+def dev_random(gpu, nbytes, seed, pad=64):
+    import torch
+    n = (nbytes + pad + 7) // 8 * 8
+    t = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    gpu._n.check(gpu._n.lib.cir_fill_splitmix64_dev(t.data_ptr(), n, seed, 0, 0, 0))
+    torch.cuda.synchronize()
+    return t
+
+
+def oracle_chunks(oracle, host, nbytes, bs):
+    nb = (nbytes + bs - 1) // bs
+    out = np.zeros(max(nb, 1) * 32, dtype=np.uint8)
+    oracle.oracle_hash_chunks(host.ctypes.data, nbytes, bs, out.ctypes.data, 8)
+    return out[:nb * 32]
+
+
+def first_bad(a, b):
+    d = (a.reshape(-1, 32) != b.reshape(-1, 32)).any(1)
+    return int(np.nonzero(d)[0][0]) if d.any() else None
+
+
+def test_golden_vectors_host_entry(ctx, vectors):
+    vecs = vectors["vectors"]
+    arena = b"".join(gen_bytes(v) for v in vecs)
+    offs, pos = [], 0
+    for v in vecs:
+        offs.append(pos)
+        pos += v["n"]
+    got = ctx.hash_blocks(arena, offs, [v["n"] for v in vecs])
+    for i, v in enumerate(vecs):
+        assert got[32 * i:32 * i + 32].hex() == v["blake2b256"], (i, v["gen"], v["n"])
+
+
+def test_golden_vectors_device_entry(gpu, ctx, vectors):
+    import torch
+    vecs = vectors["vectors"]
+    # place every vector at a 128-B aligned offset, plus misaligned copies
+    chunks, offs, lens, pos = [], [], [], 0
+    for k, v in enumerate(vecs):
+        data = gen_bytes(v)
+        skew = (k * 5) % 16 if k % 3 == 0 else 0
+        pad = (-pos) % 128 + skew
+        chunks.append(bytes(pad) + data)
+        pos += pad
+        offs.append(pos)
+        lens.append(len(data))
+        pos += len(data)
+    arena = torch.tensor(bytearray(b"".join(chunks) + bytes(16)), dtype=torch.uint8,
+                         device="cuda:0")
+    d_off = torch.tensor(offs, dtype=torch.int64, device="cuda:0")
+    d_len = torch.tensor(lens, dtype=torch.int32, device="cuda:0")
+    out = torch.zeros(32 * len(vecs), dtype=torch.uint8, device="cuda:0")
+    ctx.hash_blocks_dev(arena.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), len(vecs),
+                        out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().tobytes()
+    for i, v in enumerate(vecs):
+        assert got[32 * i:32 * i + 32].hex() == v["blake2b256"], (i, v["gen"], v["n"])
+
+
+def test_hash_bytes(gpu, oracle):
+    for data in [b"", b"abc", b"Hidden\n", bytes(128), bytes(129), os.urandom(100000)]:
+        assert bytes(gpu.BlockHash.hash_bytes(data)) == oracle_digest(oracle, data)
+
+
+@pytest.mark.parametrize("bs,nbytes", [
+    (32768, 256 * 32768),            # exactly one uniform workgroup
+    (32768, 512 * 32768 + 1000),     # uniform + short tail fused in one launch
+    (32768, 300 * 32768 + 5),        # uniform + 44 full general blocks + tail
+    (32768, 100 * 32768),            # < 256 blocks: general path only
+    (32768, 1), (32768, 127), (32768, 128), (32768, 129), (32768, 32768),
+    (4096, 1000 * 4096),
+    (128, 1024 * 128 + 64),
+    (1 << 20, 3 * (1 << 20) + 7),
+    (1000, 50000),                   # bs not a multiple of 128: unaligned blocks
+    (4097, 300001),
+    (65536, 512 * 65536),
+])
+def test_chunks_dev_vs_oracle(gpu, ctx, oracle, bs, nbytes):
+    import torch
+    data = dev_random(gpu, nbytes, seed=bs * 31 + nbytes)
+    nb = (nbytes + bs - 1) // bs
+    out = torch.zeros(nb * 32, dtype=torch.uint8, device="cuda:0")
+    ctx.hash_chunks_dev(data.data_ptr(), nbytes, bs, out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    host = data.cpu().numpy()
+    want = oracle_chunks(oracle, host, nbytes, bs)
+    got = out.cpu().numpy()
+    assert first_bad(got, want) is None, "block %s" % first_bad(got, want)
+
+
+@pytest.mark.parametrize("skew", [1, 4, 8, 15])
+def test_chunks_dev_misaligned_base(gpu, ctx, oracle, skew):
+    import torch
+    bs, nbytes = 32768, 300 * 32768 + 77
+    data = dev_random(gpu, nbytes + skew, seed=skew)
+    nb = (nbytes + bs - 1) // bs
+    out = torch.zeros(nb * 32, dtype=torch.uint8, device="cuda:0")
+    ctx.hash_chunks_dev(data.data_ptr() + skew, nbytes, bs, out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    host = data.cpu().numpy()[skew:].copy()
+    want = oracle_chunks(oracle, host, nbytes, bs)
+    assert first_bad(out.cpu().numpy(), want) is None
+
+
+def test_uniform_loaders_agree(gpu, oracle):
+    """The two uniform-kernel loaders (LDS-DMA and direct) vs the oracle."""
+    import torch
+    bs, nblk = 32768, 1024
+    data = dev_random(gpu, bs * nblk, seed=99)
+    outs = []
+    for loader in (0, 1):
+        out = torch.zeros(nblk * 32, dtype=torch.uint8, device="cuda:0")
+        gpu._n.check(gpu._n.lib.cir_debug_hash_uniform_dev(loader, data.data_ptr(), bs, nblk,
+                                                           out.data_ptr(), 0))
+        torch.cuda.synchronize()
+        outs.append(out.cpu().numpy())
+    want = oracle_chunks(oracle, data.cpu().numpy(), bs * nblk, bs)
+    assert first_bad(outs[0], want) is None
+    assert first_bad(outs[1], want) is None
+
+
+def test_desc_mixed_ragged_shuffled(gpu, ctx, oracle):
+    """Config-3 shape at small scale: 4 KiB / 32 KiB / 1 MiB classes, 10%
+    ragged, empty and boundary lengths, shuffled, some misaligned offsets."""
+    import torch
+    rng = random.Random(0x5EED0003)
+    lens = []
+    for size, count in [(4096, 3000), (32768, 400), (1 << 20, 6)]:
+        for _ in range(count):
+            lens.append(rng.randrange(1, size) if rng.random() < 0.1 else size)
+    lens += [0, 1, 127, 128, 129, 255, 256, 257, 0]
+    rng.shuffle(lens)
+    offs, pos = [], 0
+    for i, ln in enumerate(lens):
+        pos += (-pos) % 128 + (i % 7 if i % 5 == 0 else 0)
+        offs.append(pos)
+        pos += ln
+    data = dev_random(gpu, pos, seed=3)
+    d_off = torch.tensor(offs, dtype=torch.int64, device="cuda:0")
+    d_len = torch.tensor(lens, dtype=torch.int32, device="cuda:0")
+    out = torch.zeros(32 * len(lens), dtype=torch.uint8, device="cuda:0")
+    ctx.hash_blocks_dev(data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), len(lens),
+                        out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    host = data.cpu().numpy()
+    ao = np.array(offs, dtype=np.uint64)
+    al = np.array(lens, dtype=np.uint32)
+    want = np.zeros(32 * len(lens), dtype=np.uint8)
+    oracle.oracle_hash_blocks(host.ctypes.data, ao.ctypes.data, al.ctypes.data, len(lens),
+                              want.ctypes.data, 8)
+    assert first_bad(out.cpu().numpy(), want) is None
+
+
+def test_host_blocks_many_batches(small_ctx, oracle):
+    rng = random.Random(11)
+    arena = os.urandom(6 << 20)
+    n = 3000
+    lens = [rng.choice([0, 1, 100, 4096, 32768, rng.randrange(0, 70000)]) for _ in range(n)]
+    offs = [rng.randrange(0, len(arena) - ln + 1) for ln in lens]
+    got = small_ctx.hash_blocks(arena, offs, lens)
+    for i in range(n):
+        assert got[32 * i:32 * i + 32] == oracle_digest(oracle, arena[offs[i]:offs[i] + lens[i]])
+
+
+@pytest.mark.parametrize("size", [0, 1, 32767, 32768, 32769, 5 * 32768 + 3, (3 << 20) + 11])
+def test_hash_file(small_ctx, oracle, tmp_path, size):
+    data = os.urandom(size)
+    p = tmp_path / "f.bin"
+    p.write_bytes(data)
+    with open(p, "rb") as f:
+        got_size, hashes = small_ctx.hash_file(f.fileno(), 32768)
+    assert got_size == size
+    want = b"".join(oracle_digest(oracle, data[i:i + 32768]) for i in range(0, size, 32768))
+    assert hashes == want
+    assert small_ctx.hash_memory(data, 32768) == want
+
+
+def test_hashes_api(gpu, oracle, tmp_path):
+    data = os.urandom(100000)
+    p = tmp_path / "x"
+    p.write_bytes(data)
+    with open(p, "rb") as f:
+        size, hs = gpu.Hashes.hash_file(gpu.HashType.blake2b_256(), 4096, f)
+    assert size == 100000 and len(hs) == 25 and hs.block_size() == 4096
+    assert hs.get(24) == oracle_digest(oracle, data[24 * 4096:])
+
+
+def make_tree(root):
+    rng = random.Random(5)
+    (root / "a" / "b" / "c").mkdir(parents=True)
+    (root / "empty_dir").mkdir()
+    (root / "z").mkdir()
+    (root / "hello.txt").write_bytes(b"hello\n")
+    (root / "test.txt").write_bytes(b"")
+    (root / "a" / "big.bin").write_bytes(os.urandom(5 * 32768 + 1234))
+    (root / "a" / "exact.bin").write_bytes(os.urandom(2 * 32768))
+    (root / "a" / "b" / "run.sh").write_bytes(b"#!/bin/sh\necho hi\n")
+    os.chmod(root / "a" / "b" / "run.sh", 0o755)
+    (root / "a" / "b" / "c" / "deep").write_bytes(os.urandom(rng.randrange(1, 5000)))
+    for i in range(60):
+        (root / "z" / ("f%03d" % i)).write_bytes(os.urandom(rng.randrange(0, 70000)))
+    (root / "z" / "with space").write_bytes(b"x")
+    (root / "z" / "back\\slash").write_bytes(b"y")
+    os.symlink("../hello.txt", root / "a" / "link")
+    os.symlink("target with space", root / "dangling")
+
+
+def test_scan_vs_oracle(gpu, small_ctx, tmp_path):
+    make_tree(tmp_path)
+    for threads in (1, 4):
+        cfg = gpu.ScannerConfig.new().threads(threads).hash(gpu.HashType.blake2b_256())
+        cfg.add_dir(str(tmp_path), "/")
+        got = gpu.v1.scan(cfg, context=small_ctx)
+        want = dirsig_oracle.scan(str(tmp_path), 32768)
+        assert got == want
+    # block size other than the default
+    cfg = gpu.ScannerConfig.new().block_size(4096).add_dir(str(tmp_path), "/")
+    assert gpu.v1.scan(cfg, context=small_ctx) == dirsig_oracle.scan(str(tmp_path), 4096)
+
+
+def test_sync_flow_register_and_serve(gpu, small_ctx, tmp_path):
+    """scan -> register_index -> register_dir -> read_block of every block
+    (src/client/sync/uploads.rs:70-78), and the daemon-side invariant
+    BlockHash::hash_bytes(block) == index hash (fetch_blocks.rs:77)."""
+    make_tree(tmp_path)
+    cfg = gpu.ScannerConfig.new().add_dir(str(tmp_path), "/")
+    buf = bytearray()
+    gpu.v1.scan(cfg, buf, context=small_ctx)
+    index = bytes(buf)
+    idxs = gpu.InMemoryIndexes()
+    image_id = idxs.register_index(index)
+    hash_name, bs, dirs, footer = dirsig_oracle.parse(index)
+    assert bytes(image_id) == footer
+    assert footer == dirsig_oracle.h_blake2b256(index[index.index(b"\n") + 1:-65])
+    reader = gpu.ThreadedBlockReader()
+    reader.register_dir(str(tmp_path), index)
+    n = 0
+    for _, entries in dirs:
+        for e in entries:
+            if e[0] == "f":
+                for d in e[4]:
+                    block = reader.read_block(gpu.BlockHash(d), gpu.BlockHint.empty())
+                    assert bytes(gpu.BlockHash.hash_bytes(block)) == d
+                    n += 1
+    assert n >= len(reader)  # equal blocks share one entry
+
+
+def test_index_rewrite_roundtrip(gpu, small_ctx, tmp_path):
+    """RawIndex::into_mut + to_raw_data == input (the reference's own
+    `roundtrip` test, src/cluster/download.rs:368-382, on a blake2b index)."""
+    make_tree(tmp_path)
+    os.rmdir(tmp_path / "empty_dir")  # the re-emitter drops empty directories
+    cfg = gpu.ScannerConfig.new().add_dir(str(tmp_path), "/")
+    index = gpu.v1.scan(cfg, context=small_ctx)
+    assert small_ctx.index_rewrite(index) == index
+
+
+def test_memory_blocks(gpu, oracle):
+    data = os.urandom(int(2.5 * 4096))
+    r = gpu.ThreadedBlockReader()
+    r.register_memory_blocks(gpu.HashType.blake2b_256(), 4096, data)
+    assert len(r) == 3
+    for i in range(3):
+        blk = data[i * 4096:(i + 1) * 4096]
+        assert r.read_block(oracle_digest(oracle, blk)) == blk
+
+
+def test_cli_sync(gpu, tmp_path):
+    import subprocess
+    from conftest import ROOT
+    make_tree(tmp_path / "src")
+    out = subprocess.check_output([os.path.join(ROOT, "bin", "ciruela-index"), "sync",
+                                   "--append", str(tmp_path / "src") + ":/dest",
+                                   "--index-dir", str(tmp_path)])
+    image_id, kind, dest, src = out.decode().split()
+    want = dirsig_oracle.scan(str(tmp_path / "src"), 32768)
+    assert (tmp_path / (image_id + ".ds1")).read_bytes() == want
+    assert kind == "append" and dest == "/dest"
+    assert want.endswith(image_id.encode() + b"\n")

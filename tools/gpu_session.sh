@@ -1,0 +1,58 @@
+#!/bin/bash
+# One GPU session on the gpurun box: each GPU step under its own timeout,
+# stop at the first step that faults / aborts / times out (rc other than
+# 0 or 1).  Usage: tools/gpu_session.sh STEP...   (steps: smoke tests bench
+# prof pmc ubench)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+
+step() {  # name timeout cmd...
+  local name=$1 t=$2
+  shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$t" "$@"
+  local rc=$?
+  echo "== $name rc=$rc"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    echo "== stopping after $name (rc=$rc)"
+    exit $rc
+  fi
+  return 0
+}
+
+for s in "$@"; do
+  case "$s" in
+    smoke)
+      step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests)
+      step tests 900 python -m pytest tests -q -m gpu -x -p no:cacheprovider \
+        --junitxml=gpurun_out/pytest_gpu.xml > gpurun_out/pytest_gpu.log 2>&1
+      tail -5 gpurun_out/pytest_gpu.log ;;
+    bench)
+      step bench 600 python bench.py --steps 20 --warmup 3 > gpurun_out/bench.json \
+        2> gpurun_out/bench.err
+      cat gpurun_out/bench.json ;;
+    bench_direct)
+      step bench_direct 400 python bench.py --steps 10 --warmup 2 --loader direct \
+        --no-cpu-baseline > gpurun_out/bench_direct.json 2> gpurun_out/bench_direct.err
+      cat gpurun_out/bench_direct.json ;;
+    prof)
+      step prof 600 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d gpurun_out/prof -o run -- python3 bench.py --steps 10 --warmup 2 \
+        --no-cpu-baseline > gpurun_out/prof.log 2>&1
+      find gpurun_out/prof -name '*stats*' | head ;;
+    pmc)
+      for c in FETCH_SIZE WRITE_SIZE SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES \
+               SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU; do
+        step "pmc_$c" 600 rocprofv3 --pmc "$c" --output-format csv \
+          -d "gpurun_out/pmc_$c" -o run -- python3 bench.py --steps 3 --warmup 1 \
+          --no-cpu-baseline > "gpurun_out/pmc_$c.log" 2>&1
+      done ;;
+    ubench)
+      step ubench 300 ./build/valu_ubench > gpurun_out/ubench.log 2>&1
+      cat gpurun_out/ubench.log ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
