@@ -31,12 +31,23 @@ __device__ __forceinline__ uint64_t mk64(uint32_t lo, uint32_t hi) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-// rotr64(a ^ b, N) on 32-bit halves.
-template <int N>
+// rotr64(a ^ b, N) on 32-bit halves.  MODE selects the instruction form
+// (gfx950 issue costs measured by tools/valu_ubench.hip, profiles/):
+//   MODE 0: v_alignbit_b32 x2            (any N)
+//   MODE 1: v_perm_b32 x2                (N = 16, 24: byte rotates)
+//   MODE 2: (x << 1) + (x >> 63) as one v_lshl_add_u64 + v_lshrrev_b32 (N = 63)
+template <int N, int MODE>
 __device__ __forceinline__ uint64_t xor_rotr(uint64_t a, uint64_t b) {
   const uint32_t l = lo32(a) ^ lo32(b), h = hi32(a) ^ hi32(b);
   if constexpr (N == 32) {
     return mk64(h, l);
+  } else if constexpr (MODE == 1 && (N == 16 || N == 24)) {
+    // bytes of {S0, S1} numbered S1 = 0..3, S0 = 4..7; result byte k = sel[k]
+    constexpr uint32_t sel = N == 16 ? 0x05040302u : 0x06050403u;
+    return mk64(__builtin_amdgcn_perm(h, l, sel), __builtin_amdgcn_perm(l, h, sel));
+  } else if constexpr (MODE == 2 && N == 63) {
+    const uint64_t x = mk64(l, h);
+    return (x << 1) + (uint64_t)(h >> 31);
   } else if constexpr (N < 32) {
     return mk64(__builtin_amdgcn_alignbit(h, l, N), __builtin_amdgcn_alignbit(l, h, N));
   } else {
@@ -58,13 +69,13 @@ __device__ __forceinline__ uint64_t xor_rotr(uint64_t a, uint64_t b) {
 
 #define CIR_G(a, b, c, d, x, y)   \
   a = a + b + (x);                \
-  d = xor_rotr<32>(d, a);         \
+  d = xor_rotr<32, 0>(d, a);      \
   c = c + d;                      \
-  b = xor_rotr<24>(b, c);         \
+  b = xor_rotr<24, R24>(b, c);    \
   a = a + b + (y);                \
-  d = xor_rotr<16>(d, a);         \
+  d = xor_rotr<16, R16>(d, a);    \
   c = c + d;                      \
-  b = xor_rotr<63>(b, c);
+  b = xor_rotr<63, R63>(b, c);
 
 #define CIR_ROUND(s0, s1, s2, s3, s4, s5, s6, s7, s8, s9, s10, s11, s12, s13, s14, s15) \
   CIR_G(v0, v4, v8, v12, m[s0], m[s1])                                                   \
@@ -78,8 +89,10 @@ __device__ __forceinline__ uint64_t xor_rotr(uint64_t a, uint64_t b) {
 
 // F(h, m, t, f) of RFC 7693 section 3.2 with t < 2^64 (t[1] == 0: a block
 // is at most 2^32 bytes here) and f0 = last ? ~0 : 0, f1 = 0.
-__device__ __forceinline__ void compress(uint64_t h[8], const uint64_t m[16], uint64_t t,
-                                         bool last) {
+// R16 / R24 / R63: instruction form of the three non-trivial rotates.
+template <int R16, int R24, int R63>
+__device__ __forceinline__ void compress_v(uint64_t h[8], const uint64_t m[16], uint64_t t,
+                                           bool last) {
   uint64_t v0 = h[0], v1 = h[1], v2 = h[2], v3 = h[3];
   uint64_t v4 = h[4], v5 = h[5], v6 = h[6], v7 = h[7];
   uint64_t v8 = CIR_IV0, v9 = CIR_IV1, v10 = CIR_IV2, v11 = CIR_IV3;
@@ -105,6 +118,11 @@ __device__ __forceinline__ void compress(uint64_t h[8], const uint64_t m[16], ui
   h[5] ^= v5 ^ v13;
   h[6] ^= v6 ^ v14;
   h[7] ^= v7 ^ v15;
+}
+
+__device__ __forceinline__ void compress(uint64_t h[8], const uint64_t m[16], uint64_t t,
+                                         bool last) {
+  compress_v<0, 0, 0>(h, m, t, last);
 }
 
 __device__ __forceinline__ void init_state(uint64_t h[8]) {

@@ -35,22 +35,27 @@ constexpr int kWaves = kThreads / 64;
 
 // One wave hashes the 64 equal blocks starting at wsrc (bs bytes each,
 // `lines` = bs / 128 message lines) into out[0 .. 64*32).
+// Register budget: <= 96 VGPRs (5 waves per SIMD, 5 x 32 KiB LDS per CU).
+// The per-lane DMA offsets and LDS read addresses are recomputed every line
+// from one register each (one full-rate v_xor_b32 apiece) instead of being
+// hoisted into 16 + 8 registers; the DMA base address stays scalar.
 __device__ __forceinline__ void uniform_glds_wave(const uint8_t* __restrict__ wsrc, uint64_t bs,
                                                   uint32_t lines, uint8_t* __restrict__ out,
                                                   uint8_t* wl) {
   const uint32_t lane = threadIdx.x & 63u;
-  // DMA source: uniform line base (+ 8j*bs) + lane offset (r*bs + 16 chunk).
+  // DMA lane offset: r*bs + 16*chunk, chunk = (l & 7) ^ r ^ j
   const uint32_t r = lane >> 3;
-  const uint32_t dma_lane = (uint32_t)(r * bs) + 16u * ((lane & 7u) ^ r);
-  // LDS read address of chunk c: rd_base ^ 16c.
+  uint32_t dma_lane = (uint32_t)(r * bs) + 16u * ((lane & 7u) ^ r);
+  // LDS read address of chunk c: rd_base ^ 16c
   const uint32_t s = (lane ^ (lane >> 3)) & 7u;
-  const uint32_t rd_base = lane * 128u + 16u * s;
+  uint32_t rd_base = lane * 128u + 16u * s;
+  const uint64_t jstride = 8u * bs;
 
   auto issue = [&](uint32_t i) {
     const uint8_t* line = wsrc + (uint64_t)i * 128u;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const uint8_t* src = line + (uint64_t)j * 8u * bs + (dma_lane ^ (16u * j));
+      const uint8_t* src = line + (uint64_t)j * jstride + (dma_lane ^ (16u * j));
       __builtin_amdgcn_global_load_lds(
           (const void __attribute__((address_space(1)))*)src,
           (void __attribute__((address_space(3)))*)(wl + j * 1024), 16, 0, 0);
@@ -62,6 +67,8 @@ __device__ __forceinline__ void uniform_glds_wave(const uint8_t* __restrict__ ws
   uint64_t m[16];
   issue(0);
   for (uint32_t i = 0; i < lines; ++i) {
+    // opaque per iteration: keeps the derived addresses out of registers
+    asm volatile("" : "+v"(rd_base), "+v"(dma_lane));
     __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): line i landed in LDS
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
@@ -78,11 +85,11 @@ __device__ __forceinline__ void uniform_glds_wave(const uint8_t* __restrict__ ws
 }
 
 // Pure uniform launch: nblk = gridDim.x * 256 equal blocks.
-__global__ __launch_bounds__(kThreads, 4) void k_uniform_glds(const uint8_t* __restrict__ data,
+__global__ __launch_bounds__(kThreads, 5) void k_uniform_glds(const uint8_t* __restrict__ data,
                                                                uint64_t bs, uint32_t lines,
                                                                uint8_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWaves * kWaveLds];
-  const uint32_t wave = threadIdx.x >> 6;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // scalar
   const uint64_t blk0 = ((uint64_t)blockIdx.x * kWaves + wave) * 64u;
   uniform_glds_wave(data + blk0 * bs, bs, lines, out + blk0 * 32u, lds + wave * kWaveLds);
 }
@@ -93,7 +100,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_uniform_glds(const uint8_t* __r
 // loader, the others hash blocks [0, nuni) 64 per wave through LDS.  The
 // ragged workgroups come first so their chains start with the rest instead
 // of trailing the launch.
-__global__ __launch_bounds__(kThreads, 4) void k_chunks(const uint8_t* __restrict__ data,
+__global__ __launch_bounds__(kThreads, 5) void k_chunks(const uint8_t* __restrict__ data,
                                                          uint64_t nbytes, uint64_t bs,
                                                          uint32_t lines, uint64_t nuni,
                                                          uint64_t nblk, uint32_t ngen_wg,
@@ -108,7 +115,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_chunks(const uint8_t* __restric
     store_digest(out + b * 32u, h);
     return;
   }
-  const uint32_t wave = threadIdx.x >> 6;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // scalar
   const uint64_t blk0 = ((uint64_t)(blockIdx.x - ngen_wg) * kWaves + wave) * 64u;
   uniform_glds_wave(data + blk0 * bs, bs, lines, out + blk0 * 32u, lds + wave * kWaveLds);
 }

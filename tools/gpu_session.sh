@@ -24,6 +24,11 @@ step() {  # name timeout cmd...
 
 for s in "$@"; do
   case "$s" in
+    diag)
+      step diag 400 python -X faulthandler tools/diag.py ;;
+    cli)
+      head -c 100000 /dev/urandom > /tmp/cli_probe.bin
+      step cli 120 ./bin/ciruela-index hash /tmp/cli_probe.bin ;;
     smoke)
       step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests)
