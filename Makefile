@@ -15,7 +15,7 @@ OBJDIR := build/obj
 LIB := ciruela_amd/libciruela_amd.so
 CLI := bin/ciruela-index
 
-SRCS_HIP := $(CSRC)/kernels.hip
+SRCS_HIP := $(CSRC)/kernels.hip $(CSRC)/order.hip
 SRCS_CPP := $(CSRC)/runtime.cpp $(CSRC)/dirsig.cpp $(CSRC)/scan.cpp $(CSRC)/registry.cpp
 OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS_HIP)) \
         $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(SRCS_CPP))

@@ -20,6 +20,8 @@ bounded sample of the same config-2 blocks, at 4 threads (the reference's
 default --disk-threads) and at all host cores (<= 16).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--loader glds|direct]
+    python bench.py --workload config3|config5|config1   (secondary configs,
+        reported in DESIGN.md; not the headline line)
 """
 import argparse
 import ctypes
@@ -51,6 +53,10 @@ def parse():
     p.add_argument("--block-size", type=int, default=32768)
     p.add_argument("--loader", choices=["glds", "direct", "api"], default="api",
                    help="api = cir_hash_chunks_dev (production path, LDS-DMA loader)")
+    p.add_argument("--workload", choices=["auto", "config3", "config5", "config1"],
+                   default="auto", help="auto = config2 at N=1, config4 at N>1")
+    p.add_argument("--tree-gib", type=float, default=50.0, help="config5 tree size")
+    p.add_argument("--tree-dir", default="/dev/shm/ciruela_bench_tree")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=4.0,
                    help="target wall seconds per CPU-baseline measurement")
@@ -121,6 +127,133 @@ def cpu_baseline(bs, target_s):
     }
 
 
+def shard(rank, world, nblk_per_gpu):
+    """Config 4 range split: rank g owns global blocks [g*n, (g+1)*n)."""
+    return rank * nblk_per_gpu, nblk_per_gpu
+
+
+def config3_layout(total=10 << 30, seed=0x5EED0003):
+    """equal bytes per class (4 KiB / 32 KiB / 1 MiB),
+    10 % of each class ragged U[1, size-1], shuffled; blocks packed at 128-B
+    aligned offsets in descriptor order.  Returns (offsets, lengths, bytes)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    lens = []
+    for size in (4096, 32768, 1 << 20):
+        count = (total // 3) // size
+        ln = np.full(count, size, dtype=np.int64)
+        rag = rng.random(count) < 0.1
+        ln[rag] = rng.integers(1, size, size=int(rag.sum()))
+        lens.append(ln)
+    lens = np.concatenate(lens)
+    lens = lens[rng.permutation(lens.size)]
+    padded = (lens + 127) // 128 * 128
+    offs = np.zeros(lens.size, dtype=np.int64)
+    offs[1:] = np.cumsum(padded)[:-1]
+    return offs, lens.astype(np.int32), int(offs[-1] + padded[-1])
+
+
+def run_config3(args, ca, ctx, dev, stream):
+    import torch
+    offs, lens, nbytes = config3_layout()
+    data = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    ca._n.check(ca._n.lib.cir_fill_splitmix64_dev(data.data_ptr(), nbytes, 0x5EED0003, 0, 0,
+                                                  stream))
+    d_off = torch.from_numpy(offs).to(dev)
+    d_len = torch.from_numpy(lens).to(dev)
+    n = lens.size
+    out = torch.empty(32 * n, dtype=torch.uint8, device=dev)
+
+    def step():
+        ca._n.check(ca._n.lib.cir_hash_blocks_dev(ctx.handle, data.data_ptr(), d_off.data_ptr(),
+                                                  d_len.data_ptr(), n, out.data_ptr(), stream))
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    hashed = int(lens.astype("int64").sum())
+    return {"metric": "GiB/s block-hashed, config 3 (mixed 4K/32K/1M, 10% ragged, shuffled)",
+            "value": round(hashed / dt / GIB, 3), "unit": "GiB/s", "ms_per_step": round(dt * 1e3, 3),
+            "steps": args.steps, "blocks": n, "bytes": hashed,
+            "note": "includes the on-device longest-chain-first sort (order.hip)"}
+
+
+def make_tree(root, gib, file_mib=32, ndirs=40, seed=0x5EED0005):
+    """Config 5 tree: files of file_mib MiB in ndirs directories."""
+    import numpy as np
+    nfiles = int(gib * 1024 // file_mib)
+    done = os.path.join(root, ".complete-%d-%d" % (nfiles, file_mib))
+    if os.path.exists(done):
+        return nfiles
+    os.makedirs(root, exist_ok=True)
+    rng = np.random.default_rng(seed)
+    base = rng.integers(0, 1 << 63, size=file_mib * (1 << 20) // 8, dtype=np.uint64)
+    for i in range(nfiles):
+        d = os.path.join(root, "d%02d" % (i % ndirs))
+        os.makedirs(d, exist_ok=True)
+        base[0] = i  # every file (and so every first block) differs
+        base[1 + i % (base.size - 1)] ^= np.uint64(i * 0x9E3779B97F4A7C15 & ((1 << 64) - 1))
+        with open(os.path.join(d, "f%05d.bin" % i), "wb") as f:
+            f.write(base.tobytes())
+    open(done, "w").close()
+    return nfiles
+
+
+def run_config5(args, ca, ctx):
+    t0 = time.perf_counter()
+    nfiles = make_tree(args.tree_dir, args.tree_gib)
+    gen_s = time.perf_counter() - t0
+    nbytes = nfiles * 32 * (1 << 20)
+    cfg = ca.ScannerConfig.new().threads(16).add_dir(args.tree_dir, "/")
+    times = []
+    for i in range(max(1, args.steps)):
+        t0 = time.perf_counter()
+        index = ca.v1.scan(cfg, context=ctx)
+        times.append(time.perf_counter() - t0)
+    best = min(times)
+    return {"metric": "GiB/s end-to-end index of a tmpfs tree (config 5)",
+            "value": round(nbytes / best / GIB, 3), "unit": "GiB/s",
+            "seconds_best": round(best, 3), "seconds_all": [round(t, 3) for t in times],
+            "files": nfiles, "bytes": nbytes, "index_bytes": len(index),
+            "image_id": ca.get_hash(index).hex(), "tree_gen_s": round(gen_s, 1),
+            "reader_threads": 16, "tree": args.tree_dir}
+
+
+def run_config1(args, ca, ctx):
+    """100 files / 10 MiB, 10 subdirectories, through the `ciruela-index sync`
+    CLI (the indexing half of `ciruela sync --append`), plus the oracle
+    (python restatement of v1::scan) timed on the same tree."""
+    import subprocess
+    import numpy as np
+    root = "/tmp/ciruela_cfg1_tree"
+    rng = np.random.default_rng(1)
+    sizes = rng.integers(1, 2 * (10 << 20) // 100, size=100)
+    sizes = (sizes * ((10 << 20) / sizes.sum())).astype(np.int64)
+    sizes[-1] += (10 << 20) - sizes.sum()
+    for i, sz in enumerate(sizes):
+        d = os.path.join(root, "sub%d" % (i % 10))
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "file%03d" % i), "wb") as f:
+            f.write(rng.integers(0, 256, size=int(sz), dtype=np.uint8).tobytes())
+    cli = os.path.join(ROOT, "bin", "ciruela-index")
+    t0 = time.perf_counter()
+    out = subprocess.check_output([cli, "sync", "--append", root + ":/bench"])
+    cli_s = time.perf_counter() - t0
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import dirsig_oracle
+    t0 = time.perf_counter()
+    want = dirsig_oracle.scan(root)
+    oracle_s = time.perf_counter() - t0
+    image_id = out.decode().split()[0]
+    return {"metric": "config 1: 100-file / 10 MiB tree via `ciruela-index sync --append`",
+            "cli_seconds": round(cli_s, 3), "oracle_python_seconds": round(oracle_s, 3),
+            "image_id": image_id, "matches_oracle": want.endswith(image_id.encode() + b"\n")}
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -144,6 +277,15 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
     ctx = ca.Context(device_mask=1 << local)
 
+    if args.workload != "auto":
+        if world != 1:
+            raise SystemExit("secondary workloads run on one GPU")
+        rec = {"config3": lambda: run_config3(args, ca, ctx, dev, stream),
+               "config5": lambda: run_config5(args, ca, ctx),
+               "config1": lambda: run_config1(args, ca, ctx)}[args.workload]()
+        print(json.dumps(rec), flush=True)
+        return 0
+
     data = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     out = torch.empty(nblk * 32, dtype=torch.uint8, device=dev)
     if world == 1:
@@ -151,8 +293,9 @@ def main():
         fill_config2(ca, data, bs, stream)
     else:
         workload = "config4"
+        first, _ = shard(rank, world, nblk)
         ca._n.check(ca._n.lib.cir_fill_splitmix64_dev(data.data_ptr(), nbytes, SEED_C4, bs,
-                                                      rank * nblk, stream))
+                                                      first, stream))
     torch.cuda.synchronize()
 
     lib = ca._n.lib

@@ -30,6 +30,12 @@ hipError_t launch_general_chunks(const uint8_t* data, uint64_t nbytes, uint64_t 
 hipError_t launch_general_desc(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
                                const uint32_t* perm, uint64_t n, uint8_t* out, hipStream_t s);
 
+// Longest-chain-first order of a descriptor batch (order.hip): *perm points
+// into `scratch` (order_scratch_bytes(n) bytes, device memory).
+size_t order_scratch_bytes(uint64_t n);
+hipError_t launch_order_desc(const uint32_t* len, uint64_t n, void* scratch, size_t bytes,
+                             uint32_t** perm, hipStream_t s);
+
 hipError_t launch_fill_splitmix64(uint64_t* p, uint64_t nwords, uint64_t seed,
                                   uint64_t block_words, uint64_t first_block, hipStream_t s);
 

@@ -1,0 +1,53 @@
+// Processing order of a mixed-length descriptor batch (config 3).
+//
+// One lane hashes one block, so a wave costs as much as its longest chain.
+// Sorting descriptors by compression count (descending) puts chains of equal
+// length in the same waves and dispatches the longest ones first, so they
+// overlap with the short ones instead of trailing the launch.  The sort runs
+// on the device (hipCUB radix sort on 26-bit keys) inside the timed call.
+#include <hipcub/hipcub.hpp>
+
+#include "kernels.hpp"
+
+namespace cir {
+namespace dev {
+
+__global__ void k_chain_keys(const uint32_t* __restrict__ len, uint64_t n,
+                             uint32_t* __restrict__ key, uint32_t* __restrict__ idx) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t l = len[i];
+  key[i] = l == 0 ? 1u : (l >> 7) + ((l & 127u) != 0);  // compressions, <= 2^25
+  idx[i] = (uint32_t)i;
+}
+
+size_t order_scratch_bytes(uint64_t n) {
+  size_t temp = 0;
+  (void)hipcub::DeviceRadixSort::SortPairsDescending(nullptr, temp, (const uint32_t*)nullptr,
+                                                     (uint32_t*)nullptr, (const uint32_t*)nullptr,
+                                                     (uint32_t*)nullptr, (int)n, 0, 26);
+  return ((temp + 255) & ~(size_t)255) + 4 * ((n * 4 + 255) & ~(uint64_t)255);
+}
+
+hipError_t launch_order_desc(const uint32_t* len, uint64_t n, void* scratch, size_t bytes,
+                             uint32_t** perm, hipStream_t s) {
+  const uint64_t arr = (n * 4 + 255) & ~(uint64_t)255;
+  uint8_t* p = static_cast<uint8_t*>(scratch);
+  uint32_t* key_in = reinterpret_cast<uint32_t*>(p);
+  uint32_t* key_out = reinterpret_cast<uint32_t*>(p + arr);
+  uint32_t* idx_in = reinterpret_cast<uint32_t*>(p + 2 * arr);
+  uint32_t* idx_out = reinterpret_cast<uint32_t*>(p + 3 * arr);
+  void* temp = p + 4 * arr;
+  size_t temp_bytes = bytes - 4 * arr;
+  hipLaunchKernelGGL(k_chain_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, len, n,
+                     key_in, idx_in);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = hipcub::DeviceRadixSort::SortPairsDescending(temp, temp_bytes, key_in, key_out, idx_in,
+                                                   idx_out, (int)n, 0, 26, s);
+  *perm = idx_out;
+  return e;
+}
+
+}  // namespace dev
+}  // namespace cir

@@ -42,6 +42,9 @@ Device::~Device() {
     if (s.copied) (void)hipEventDestroy(s.copied);
     if (s.done) (void)hipEventDestroy(s.done);
   }
+  if (order_free) (void)hipEventSynchronize(order_free);
+  (void)hipFree(order_scratch);
+  if (order_free) (void)hipEventDestroy(order_free);
   if (compute) (void)hipStreamDestroy(compute);
   if (copy) (void)hipStreamDestroy(copy);
 }
@@ -86,6 +89,33 @@ int Device::ensure_slot(Slot& s, uint64_t bytes, uint64_t nblk) {
   return CIR_OK;
 }
 
+// Descriptor batch, longest chain first: device sort (order.hip) into the
+// device's ordering scratch, then the general kernel through the permutation.
+int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, const uint32_t* len,
+                      uint64_t n, uint8_t* out, hipStream_t s) {
+  if (n <= 4 * (uint64_t)dev::kThreads) {
+    CIR_HIP(dev::launch_general_desc(arena, off, len, nullptr, n, out, s));
+    return CIR_OK;
+  }
+  std::lock_guard<std::mutex> lk(d.order_mu);
+  const size_t need = dev::order_scratch_bytes(n);
+  if (!d.order_free) CIR_HIP(hipEventCreateWithFlags(&d.order_free, hipEventDisableTiming));
+  if (need > d.order_cap) {
+    CIR_HIP(hipEventSynchronize(d.order_free));
+    (void)hipFree(d.order_scratch);
+    d.order_scratch = nullptr;
+    d.order_cap = 0;
+    CIR_HIP(hipMalloc(&d.order_scratch, need));
+    d.order_cap = need;
+  }
+  CIR_HIP(hipStreamWaitEvent(s, d.order_free, 0));
+  uint32_t* perm = nullptr;
+  CIR_HIP(dev::launch_order_desc(len, n, d.order_scratch, d.order_cap, &perm, s));
+  CIR_HIP(dev::launch_general_desc(arena, off, len, perm, n, out, s));
+  CIR_HIP(hipEventRecord(d.order_free, s));
+  return CIR_OK;
+}
+
 // Upload a packed slot and hash it.  chunk_bs == 0: descriptor batch
 // (h_off/h_len, nblk blocks); otherwise the slot holds `bytes` consecutive
 // bytes of one file split into chunk_bs blocks (nblk = ceil(bytes / bs)).
@@ -98,10 +128,10 @@ static int slot_submit_impl(Device& d, Slot& s, uint64_t bytes, uint64_t nblk,
   }
   CIR_HIP(hipEventRecord(s.copied, d.copy));
   CIR_HIP(hipStreamWaitEvent(d.compute, s.copied, 0));
-  if (chunk_bs == 0)
-    CIR_HIP(dev::launch_general_desc(s.d_data, s.d_off, s.d_len, nullptr, nblk, s.d_out,
-                                     d.compute));
-  else
+  if (chunk_bs == 0) {
+    int rc = hash_desc_ordered(d, s.d_data, s.d_off, s.d_len, nblk, s.d_out, d.compute);
+    if (rc) return rc;
+  } else
     CIR_HIP(dev::launch_chunks(s.d_data, bytes, chunk_bs, s.d_out, d.compute));
   CIR_HIP(hipMemcpyAsync(s.h_out, s.d_out, nblk * 32, hipMemcpyDeviceToHost, d.compute));
   CIR_HIP(hipEventRecord(s.done, d.compute));
@@ -361,11 +391,25 @@ int cir_hash_chunks_dev(cir_ctx* ctx, const void* d_data, uint64_t nbytes, uint6
 
 int cir_hash_blocks_dev(cir_ctx* ctx, const void* d_arena, const uint64_t* d_off,
                         const uint32_t* d_len, size_t nblk, uint8_t* d_out, void* stream) {
-  (void)ctx;
   if (nblk && (!d_arena || !d_off || !d_len || !d_out))
     return fail(CIR_EINVAL, "null device pointer");
-  CIR_HIP(dev::launch_general_desc((const uint8_t*)d_arena, d_off, d_len, nullptr, nblk, d_out,
-                                   (hipStream_t)stream));
+  if (nblk > 0xffffffffull) return fail(CIR_EINVAL, "more than 2^32 descriptors");
+  hipStream_t s = (hipStream_t)stream;
+  // Small batches and context-less calls hash in descriptor order; the rest
+  // are ordered longest chain first on the device (order.hip).
+  if (ctx && nblk > 4 * (size_t)dev::kThreads) {
+    int id = 0;
+    if (s)
+      CIR_HIP(hipStreamGetDevice(s, &id));
+    else
+      CIR_HIP(hipGetDevice(&id));
+    Device* d = nullptr;
+    for (auto& p : ctx->devs)
+      if (p->id == id) d = p.get();
+    if (!d) return fail(CIR_EINVAL, "stream device is not part of the context");
+    return hash_desc_ordered(*d, (const uint8_t*)d_arena, d_off, d_len, nblk, d_out, s);
+  }
+  CIR_HIP(dev::launch_general_desc((const uint8_t*)d_arena, d_off, d_len, nullptr, nblk, d_out, s));
   return CIR_OK;
 }
 

@@ -49,6 +49,12 @@ struct Device {
   hipStream_t copy = nullptr;
   Slot slot[2];
   std::mutex mu;  // one host-path user at a time per device
+  // device scratch of the descriptor ordering (cir_hash_blocks_dev); users on
+  // different streams are ordered through `order_free`.
+  std::mutex order_mu;
+  void* order_scratch = nullptr;
+  size_t order_cap = 0;
+  hipEvent_t order_free = nullptr;
   ~Device();
   int ensure_slot(Slot& s, uint64_t bytes, uint64_t nblk);
 };
@@ -58,6 +64,8 @@ struct Device {
 // Staging engine: the caller packs a slot, submit() uploads and hashes it
 // asynchronously, wait() returns the digests in h_out.
 int slot_submit(Device& d, Slot& s, uint64_t bytes, uint64_t nblk);
+int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, const uint32_t* len,
+                      uint64_t n, uint8_t* out, hipStream_t s);
 int slot_wait(Device& d, Slot& s);
 
 }  // namespace cir

@@ -1,0 +1,91 @@
+"""The N > 1 bench path on CPU: world_size-2 `gloo` processes.
+
+The block hash shards with no data-path collective: rank g
+owns global blocks [g*n, (g+1)*n) of config 4, each block its own splitmix64
+stream (seed 0x5EED0004 ^ global index).  Checked here without a GPU:
+  * the shards are disjoint and cover [0, world*n);
+  * every rank regenerates its blocks from the global index alone, so a
+    block's digest does not depend on which rank hashed it (oracle digests of
+    boundary blocks computed on both sides agree);
+  * the timing reduction is a MAX over ranks (bench.py's all_reduce).
+"""
+import ctypes
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+SEED_C4 = 0x5EED0004
+BS = 4096  # small blocks: the property does not depend on the size
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _oracle():
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "liboracle_blake2b.so"))
+    vp, u64 = ctypes.c_void_p, ctypes.c_uint64
+    lib.oracle_hash_chunks.argtypes = [vp, u64, u64, vp, ctypes.c_int]
+    lib.oracle_splitmix64_fill.argtypes = [vp, u64, u64, u64, u64, u64]
+    return lib
+
+
+def _worker(rank, world, port, nblk, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    first, count = bench.shard(rank, world, nblk)
+    lib = _oracle()
+    # this rank's shard, generated exactly as bench.py fills HBM (per-block seeds)
+    buf = np.empty(count * BS // 8, dtype=np.uint64)
+    lib.oracle_splitmix64_fill(buf.ctypes.data, 0, buf.size, SEED_C4, BS // 8, first)
+    dig = np.empty(count * 32, dtype=np.uint8)
+    lib.oracle_hash_chunks(buf.ctypes.data, count * BS, BS, dig.ctypes.data, 1)
+    # gather shard bounds and the digest of every rank's first block
+    t = torch.tensor([first, count] + list(dig[:32].astype(np.int64)), dtype=torch.int64)
+    parts = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    elapsed = torch.tensor([0.1 * (rank + 1)], dtype=torch.float64)
+    dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        q.put(([p.tolist() for p in parts], float(elapsed.item())))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_range_split_gloo(world):
+    nblk = 64
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, nblk, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    parts, elapsed = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    bounds = sorted((p[0], p[1]) for p in parts)
+    assert bounds[0][0] == 0
+    for (a, n), (b, _) in zip(bounds, bounds[1:]):
+        assert a + n == b  # contiguous, disjoint
+    assert bounds[-1][0] + bounds[-1][1] == world * nblk
+    assert elapsed == pytest.approx(0.1 * world)  # max over ranks
+    # the first block of rank 1 == global block nblk, regenerated from scratch here
+    lib = _oracle()
+    buf = np.empty(BS // 8, dtype=np.uint64)
+    lib.oracle_splitmix64_fill(buf.ctypes.data, 0, buf.size, SEED_C4, BS // 8, nblk)
+    dig = np.empty(32, dtype=np.uint8)
+    lib.oracle_hash_chunks(buf.ctypes.data, BS, BS, dig.ctypes.data, 1)
+    assert [int(x) for x in dig] == parts[1][2:]

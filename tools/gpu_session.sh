@@ -55,6 +55,20 @@ for s in "$@"; do
           -d "gpurun_out/pmc_$c" -o run -- python3 bench.py --steps 3 --warmup 1 \
           --no-cpu-baseline > "gpurun_out/pmc_$c.log" 2>&1
       done ;;
+    cfg3)
+      step cfg3 600 python bench.py --workload config3 --steps 5 --warmup 1 \
+        > gpurun_out/cfg3.json 2> gpurun_out/cfg3.err
+      cat gpurun_out/cfg3.json ;;
+    cfg1)
+      step cfg1 300 python bench.py --workload config1 > gpurun_out/cfg1.json 2> gpurun_out/cfg1.err
+      cat gpurun_out/cfg1.json ;;
+    cfg5)
+      df -h /dev/shm /tmp | tee gpurun_out/df.txt
+      free -g | tee -a gpurun_out/df.txt
+      step cfg5 1000 python bench.py --workload config5 --steps 3 --tree-gib "${TREE_GIB:-50}" \
+        > gpurun_out/cfg5.json 2> gpurun_out/cfg5.err
+      rm -rf /dev/shm/ciruela_bench_tree
+      cat gpurun_out/cfg5.json ;;
     ubench)
       step ubench 300 ./build/valu_ubench > gpurun_out/ubench.log 2>&1
       cat gpurun_out/ubench.log ;;
