@@ -1,0 +1,69 @@
+"""Pin the DIRSIGNATURE.v1 oracle with the reference's own fixture (CPU).
+
+Fixture: src/cluster/download.rs:357-366 (test `roundtrip`), the only index
+in the reference.  It is sha512/256, so it pins the format and the footer
+rule, not the blake2b hash (that is pinned in test_oracle.py).
+"""
+import hashlib
+import os
+
+import dirsig_oracle
+import ciruela_amd as ca
+
+
+def test_fixture_facts(dirsig_example):
+    idx = dirsig_example["index"].encode()
+    header_end = idx.index(b"\n") + 1
+    body = idx[header_end:-65]
+    # footer = H(every byte after the header line), newline included
+    assert hashlib.new("sha512_256", body).hexdigest().encode() == idx[-65:-1]
+    # per-block hash = H(block bytes)
+    assert hashlib.new("sha512_256", b"Hidden\n").hexdigest() == \
+        "6d7f5f9804ee4dbc1ff7e12c7665387e0119e8ea629996c52d38b75c12ad0acf"
+
+
+def test_oracle_emitter_reproduces_fixture(dirsig_example):
+    idx = dirsig_example["index"].encode()
+    hash_name, bs, dirs, footer = dirsig_oracle.parse(idx)
+    assert (hash_name, bs) == ("sha512/256", 32768)
+    assert dirsig_oracle.emit(hash_name, bs, dirs) == idx
+
+
+def test_oracle_block_split():
+    data = os.urandom(70000)
+    hs = dirsig_oracle.block_hashes(data, 32768)
+    assert len(hs) == 3
+    assert hs[2] == hashlib.blake2b(data[65536:], digest_size=32).digest()
+    assert dirsig_oracle.block_hashes(b"", 32768) == []
+
+
+def test_oracle_scan_small_tree(tmp_path):
+    (tmp_path / "b").mkdir()
+    (tmp_path / "a.txt").write_bytes(b"hello\n")
+    (tmp_path / "b" / ".hidden").write_bytes(b"Hidden\n")
+    (tmp_path / "b" / "empty").write_bytes(b"")
+    idx = dirsig_oracle.scan(str(tmp_path))
+    lines = idx.split(b"\n")
+    assert lines[0] == b"DIRSIGNATURE.v1 blake2b/256 block_size=32768"
+    assert lines[1] == b"/"
+    assert lines[2].startswith(b"  a.txt f 6 ")
+    assert lines[3] == b"/b"
+    assert lines[4].startswith(b"  .hidden f 7 ")
+    assert lines[5] == b"  empty f 0"
+    assert lines[6] == hashlib.blake2b(b"\n".join(lines[1:6]) + b"\n",
+                                       digest_size=32).hexdigest().encode()
+
+
+def test_escape():
+    assert dirsig_oracle.escape(b"a b\\c\x7f\xff") == b"a\\x20b\\x5cc\\x7f\\xff"
+
+
+def test_library_parser_on_fixture(dirsig_example, tmp_path):
+    """The product's parser accepts the fixture (sha512/256 parses; only
+    hashing it is GPU-unsupported) and maps every block (register_dir)."""
+    idx = dirsig_example["index"].encode()
+    assert ca.get_hash(idx) == bytes.fromhex(
+        "552ca5730ee95727e890a2155c88609d244624034ff70de264cf88220d11d6df")
+    r = ca.ThreadedBlockReader()
+    r.register_dir(str(tmp_path), idx)
+    assert len(r) == 3
