@@ -14,6 +14,8 @@
 // and BlockHash::hash_bytes (src/block_id.rs:37-43).
 #include "kernels.hpp"
 
+#include <algorithm>
+
 #include "blake2b_dev.hpp"
 
 namespace cir {
@@ -167,6 +169,109 @@ __global__ __launch_bounds__(kThreads, 4) void k_general(const uint8_t* __restri
   store_digest(out + b * 32u, h);
 }
 
+// ---------------------------------------------------------------------------
+// Mixed-length descriptor batch, ordered longest chain first (order.hip):
+// workgroups [0, nq_wg) run quad-per-chain mode (4 lanes per chain, 16 chains
+// per wave, s_setprio 3) over the first min(*n_long, 64 nq_wg) chains; the
+// rest run lane-per-chain over the remaining ones.  One launch, so the long
+// chains start first and the short ones fill the machine around them.
+// ---------------------------------------------------------------------------
+__constant__ uint8_t kSigma[12][16] = {
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+    {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+    {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4},
+    {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+    {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13},
+    {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+    {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11},
+    {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+    {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5},
+    {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+    {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
+
+constexpr int kQuadWaveLds = 16 * 128;  // one 128-B line per quad
+
+__device__ __forceinline__ void quad_chains(const uint8_t* __restrict__ arena,
+                                            const uint64_t* __restrict__ off,
+                                            const uint32_t* __restrict__ len,
+                                            const uint32_t* __restrict__ perm, uint32_t first,
+                                            uint32_t nlong, uint8_t* __restrict__ out,
+                                            uint8_t* lds, uint32_t wave_lds) {
+  const uint32_t lane = threadIdx.x & 63u, i = lane & 3u, q = lane >> 2;
+  const uint32_t c = first + q;
+  const bool have = c < nlong;
+  uint32_t b = 0, L = 0;
+  uint64_t o = 0;
+  if (have) {
+    b = perm[c];
+    o = off[b];
+    L = len[b];
+  }
+  const uint8_t* p = arena + o;
+  const uint32_t line = wave_lds + q * 128u;  // this quad's line in LDS
+  uint32_t addr[48];
+#pragma unroll
+  for (int r = 0; r < 12; ++r) {
+    addr[4 * r + 0] = line + 8u * kSigma[r][2 * i];
+    addr[4 * r + 1] = line + 8u * kSigma[r][2 * i + 1];
+    addr[4 * r + 2] = line + 8u * kSigma[r][8 + 2 * i];
+    addr[4 * r + 3] = line + 8u * kSigma[r][9 + 2 * i];
+  }
+  const uint32_t nfull = L >> 7, rem = L & 127u;
+  const uint32_t total = have ? nfull + ((rem != 0u || L == 0u) ? 1u : 0u) : 0u;
+  const bool al16 = (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+  const uint64_t ivc[4] = {CIR_IV0, CIR_IV1, CIR_IV2, CIR_IV3};
+  const uint64_t ivd[4] = {CIR_IV4, CIR_IV5, CIR_IV6, CIR_IV7};
+  const uint64_t cv = i == 0 ? ivc[0] : i == 1 ? ivc[1] : i == 2 ? ivc[2] : ivc[3];
+  const uint64_t dv0 = i == 0 ? ivd[0] : i == 1 ? ivd[1] : i == 2 ? ivd[2] : ivd[3];
+  uint64_t h0 = i == 0 ? cv ^ CIR_P0_256 : cv;
+  uint64_t h1 = dv0;
+  auto fetch = [&](uint32_t it, uint4& u, uint4& w) {
+    const uint32_t lb = it < nfull ? 128u : rem;
+    const uint32_t n = lb > 32u * i ? min(32u, lb - 32u * i) : 0u;
+    load32_safe(u, w, p + (uint64_t)it * 128u + 32u * i, n, al16);
+  };
+  uint4 u = make_uint4(0, 0, 0, 0), w = u;
+  if (total) fetch(0, u, w);
+  for (uint32_t it = 0; it < total; ++it) {
+    // publish this lane's 32 bytes of the line to its quad (LDS is in order
+    // per wave: the previous compression's reads precede these writes)
+    *reinterpret_cast<uint4*>(lds + line + 32u * i) = u;
+    *reinterpret_cast<uint4*>(lds + line + 32u * i + 16u) = w;
+    if (it + 1 < total) fetch(it + 1, u, w);
+    const bool last = it + 1 == total;
+    const uint64_t t = last ? (uint64_t)L : (uint64_t)(it + 1) * 128u;
+    const uint64_t dv = dv0 ^ (i == 0 ? t : 0ull) ^ ((i == 2 && last) ? ~0ull : 0ull);
+    compress_quad(h0, h1, lds, addr, cv, dv);
+  }
+  if (have) *reinterpret_cast<uint64_t*>(out + (uint64_t)b * 32u + 8u * i) = h0;
+}
+
+__global__ __launch_bounds__(kThreads, 4) void k_mixed(const uint8_t* __restrict__ arena,
+                                                        const uint64_t* __restrict__ off,
+                                                        const uint32_t* __restrict__ len,
+                                                        const uint32_t* __restrict__ perm,
+                                                        uint64_t n, const uint32_t* n_long,
+                                                        uint32_t nq_wg, uint8_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kWaves * kQuadWaveLds];
+  const uint32_t nl = min(*n_long, nq_wg * 64u);
+  if (blockIdx.x < nq_wg) {
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t first = (blockIdx.x * kWaves + wave) * 16u;
+    if (first >= nl) return;
+    __builtin_amdgcn_s_setprio(3);
+    quad_chains(arena, off, len, perm, first, nl, out, lds, wave * kQuadWaveLds);
+    return;
+  }
+  const uint64_t j = nl + (uint64_t)(blockIdx.x - nq_wg) * kThreads + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t b = perm[j];
+  uint64_t h[8];
+  hash_chain(arena + off[b], len[b], h);
+  store_digest(out + (uint64_t)b * 32u, h);
+}
+
 __device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t k) {
   uint64_t z = seed + (k + 1) * 0x9e3779b97f4a7c15ULL;
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
@@ -238,6 +343,18 @@ hipError_t launch_general_desc(const uint8_t* arena, const uint64_t* off, const 
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_general, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, arena,
                      (uint64_t)0, (uint64_t)0, (uint64_t)0, off, len, perm, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
+                        const uint32_t* perm, const uint32_t* n_long, uint64_t n, uint8_t* out,
+                        hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint64_t nq = std::min<uint64_t>((n + 63) / 64, (uint64_t)kQuadMaxWg);
+  const uint64_t grid = nq + grid_for(n, kThreads);
+  if (grid > 0x7fffffffull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_mixed, dim3((unsigned)grid), dim3(kThreads), 0, s, arena, off, len, perm, n,
+                     n_long, (uint32_t)nq, out);
   return hipGetLastError();
 }
 

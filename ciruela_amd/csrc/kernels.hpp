@@ -10,6 +10,10 @@ constexpr int kThreads = 256;  // 4 waves per workgroup
 
 enum class Loader : int { kGlds = 0, kDirect = 1 };
 
+// Chains of at least this many 128-B lines (256 KiB) run 4 lanes per chain.
+constexpr uint32_t kQuadMinLines = 2048;
+constexpr int kQuadMaxWg = 256;  // at most 256 x 64 = 16384 chains in quad mode
+
 // nblk equal blocks of bs bytes at data (bs % 128 == 0, data 16-byte aligned,
 // nblk % 256 == 0).  out: nblk x 32 bytes.
 hipError_t launch_uniform(Loader loader, const uint8_t* data, uint64_t bs, uint64_t nblk,
@@ -30,11 +34,18 @@ hipError_t launch_general_chunks(const uint8_t* data, uint64_t nbytes, uint64_t 
 hipError_t launch_general_desc(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
                                const uint32_t* perm, uint64_t n, uint8_t* out, hipStream_t s);
 
+// Descriptor batch in the order perm (longest chain first); the first
+// min(*n_long, 64 * kQuadMaxWg) chains (device count) run in quad mode.
+hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
+                        const uint32_t* perm, const uint32_t* n_long, uint64_t n, uint8_t* out,
+                        hipStream_t s);
+
 // Longest-chain-first order of a descriptor batch (order.hip): *perm points
 // into `scratch` (order_scratch_bytes(n) bytes, device memory).
 size_t order_scratch_bytes(uint64_t n);
+// *n_long = number of chains with >= kQuadMinLines lines (device memory).
 hipError_t launch_order_desc(const uint32_t* len, uint64_t n, void* scratch, size_t bytes,
-                             uint32_t** perm, hipStream_t s);
+                             uint32_t** perm, uint32_t** n_long, hipStream_t s);
 
 hipError_t launch_fill_splitmix64(uint64_t* p, uint64_t nwords, uint64_t seed,
                                   uint64_t block_words, uint64_t first_block, hipStream_t s);

@@ -13,12 +13,15 @@ namespace cir {
 namespace dev {
 
 __global__ void k_chain_keys(const uint32_t* __restrict__ len, uint64_t n,
-                             uint32_t* __restrict__ key, uint32_t* __restrict__ idx) {
+                             uint32_t* __restrict__ key, uint32_t* __restrict__ idx,
+                             uint32_t* __restrict__ n_long) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t l = len[i];
-  key[i] = l == 0 ? 1u : (l >> 7) + ((l & 127u) != 0);  // compressions, <= 2^25
+  const uint32_t k = l == 0 ? 1u : (l >> 7) + ((l & 127u) != 0);  // compressions, <= 2^25
+  key[i] = k;
   idx[i] = (uint32_t)i;
+  if (k >= kQuadMinLines) atomicAdd(n_long, 1u);
 }
 
 size_t order_scratch_bytes(uint64_t n) {
@@ -26,13 +29,18 @@ size_t order_scratch_bytes(uint64_t n) {
   (void)hipcub::DeviceRadixSort::SortPairsDescending(nullptr, temp, (const uint32_t*)nullptr,
                                                      (uint32_t*)nullptr, (const uint32_t*)nullptr,
                                                      (uint32_t*)nullptr, (int)n, 0, 26);
-  return ((temp + 255) & ~(size_t)255) + 4 * ((n * 4 + 255) & ~(uint64_t)255);
+  return 256 + ((temp + 255) & ~(size_t)255) + 4 * ((n * 4 + 255) & ~(uint64_t)255);
 }
 
 hipError_t launch_order_desc(const uint32_t* len, uint64_t n, void* scratch, size_t bytes,
-                             uint32_t** perm, hipStream_t s) {
+                             uint32_t** perm, uint32_t** n_long, hipStream_t s) {
   const uint64_t arr = (n * 4 + 255) & ~(uint64_t)255;
-  uint8_t* p = static_cast<uint8_t*>(scratch);
+  uint32_t* count = static_cast<uint32_t*>(scratch);
+  uint8_t* p = static_cast<uint8_t*>(scratch) + 256;
+  bytes -= 256;
+  hipError_t e0 = hipMemsetAsync(count, 0, 4, s);
+  if (e0 != hipSuccess) return e0;
+  *n_long = count;
   uint32_t* key_in = reinterpret_cast<uint32_t*>(p);
   uint32_t* key_out = reinterpret_cast<uint32_t*>(p + arr);
   uint32_t* idx_in = reinterpret_cast<uint32_t*>(p + 2 * arr);
@@ -40,7 +48,7 @@ hipError_t launch_order_desc(const uint32_t* len, uint64_t n, void* scratch, siz
   void* temp = p + 4 * arr;
   size_t temp_bytes = bytes - 4 * arr;
   hipLaunchKernelGGL(k_chain_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, len, n,
-                     key_in, idx_in);
+                     key_in, idx_in, count);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   e = hipcub::DeviceRadixSort::SortPairsDescending(temp, temp_bytes, key_in, key_out, idx_in,

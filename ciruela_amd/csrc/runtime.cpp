@@ -110,8 +110,9 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
   }
   CIR_HIP(hipStreamWaitEvent(s, d.order_free, 0));
   uint32_t* perm = nullptr;
-  CIR_HIP(dev::launch_order_desc(len, n, d.order_scratch, d.order_cap, &perm, s));
-  CIR_HIP(dev::launch_general_desc(arena, off, len, perm, n, out, s));
+  uint32_t* n_long = nullptr;
+  CIR_HIP(dev::launch_order_desc(len, n, d.order_scratch, d.order_cap, &perm, &n_long, s));
+  CIR_HIP(dev::launch_mixed(arena, off, len, perm, n_long, n, out, s));
   CIR_HIP(hipEventRecord(d.order_free, s));
   return CIR_OK;
 }
