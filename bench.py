@@ -208,7 +208,8 @@ def run_config5(args, ca, ctx):
     nfiles = make_tree(args.tree_dir, args.tree_gib)
     gen_s = time.perf_counter() - t0
     nbytes = nfiles * 32 * (1 << 20)
-    cfg = ca.ScannerConfig.new().threads(16).add_dir(args.tree_dir, "/")
+    threads = int(os.environ.get("CIR_SCAN_THREADS", "16"))
+    cfg = ca.ScannerConfig.new().threads(threads).add_dir(args.tree_dir, "/")
     times = []
     for i in range(max(1, args.steps)):
         t0 = time.perf_counter()
@@ -220,7 +221,7 @@ def run_config5(args, ca, ctx):
             "seconds_best": round(best, 3), "seconds_all": [round(t, 3) for t in times],
             "files": nfiles, "bytes": nbytes, "index_bytes": len(index),
             "image_id": ca.get_hash(index).hex(), "tree_gen_s": round(gen_s, 1),
-            "reader_threads": 16, "tree": args.tree_dir}
+            "reader_threads": threads, "tree": args.tree_dir}
 
 
 def run_config1(args, ca, ctx):

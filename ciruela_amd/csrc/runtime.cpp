@@ -93,10 +93,9 @@ int Device::ensure_slot(Slot& s, uint64_t bytes, uint64_t nblk) {
 // device's ordering scratch, then the general kernel through the permutation.
 int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, const uint32_t* len,
                       uint64_t n, uint8_t* out, hipStream_t s) {
-  if (n <= 4 * (uint64_t)dev::kThreads) {
-    CIR_HIP(dev::launch_general_desc(arena, off, len, nullptr, n, out, s));
-    return CIR_OK;
-  }
+  // Every batch is ordered (even a single chain: an index footer is one long
+  // chain and runs in quad mode).
+  if (n == 0) return CIR_OK;
   std::lock_guard<std::mutex> lk(d.order_mu);
   const size_t need = dev::order_scratch_bytes(n);
   if (!d.order_free) CIR_HIP(hipEventCreateWithFlags(&d.order_free, hipEventDisableTiming));
@@ -396,9 +395,10 @@ int cir_hash_blocks_dev(cir_ctx* ctx, const void* d_arena, const uint64_t* d_off
     return fail(CIR_EINVAL, "null device pointer");
   if (nblk > 0xffffffffull) return fail(CIR_EINVAL, "more than 2^32 descriptors");
   hipStream_t s = (hipStream_t)stream;
-  // Small batches and context-less calls hash in descriptor order; the rest
-  // are ordered longest chain first on the device (order.hip).
-  if (ctx && nblk > 4 * (size_t)dev::kThreads) {
+  // Context-less calls hash in descriptor order, one lane per chain; with a
+  // context the batch is ordered longest chain first on the device
+  // (order.hip) and long chains run in quad mode.
+  if (ctx) {
     int id = 0;
     if (s)
       CIR_HIP(hipStreamGetDevice(s, &id));

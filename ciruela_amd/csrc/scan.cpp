@@ -13,6 +13,7 @@
 // a directory line, its files and symlinks sorted by name (bytewise), then
 // its subdirectories recursively in name order.
 #include <dirent.h>
+#include <stdio.h>
 #include <errno.h>
 #include <fcntl.h>
 #include <string.h>
@@ -21,6 +22,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdlib>
 #include <map>
 #include <memory>
 #include <thread>
@@ -97,6 +100,21 @@ static int walk(const std::string& real, const std::string& vpath, std::vector<P
     if (rc) return rc;
   }
   return CIR_OK;
+}
+
+// Read jobs are cut into pieces of at most this size so that `threads`
+// readers stay busy on trees of large files.
+constexpr uint64_t kReadPiece = 4ull << 20;
+
+static bool trace_on() {
+  static const bool on = std::getenv("CIR_TRACE") != nullptr;
+  return on;
+}
+
+static double now_ms() {
+  return std::chrono::duration<double, std::milli>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
 }
 
 struct ReadJob {
@@ -184,11 +202,13 @@ static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, u
   };
   while (more() || d.slot[0].busy || d.slot[1].busy) {
     Slot& s = d.slot[k];
+    const double t_wait0 = trace_on() ? now_ms() : 0;
     if (s.busy) {
       int rc = slot_wait(d, s);
       if (rc) return rc;
       memcpy(digests.data() + 32 * pending_first[k], s.h_out, 32 * pending_n[k]);
     }
+    const double t_wait1 = trace_on() ? now_ms() : 0;
     if (more()) {
       int rc = d.ensure_slot(s, cap, cap_blk);
       if (rc) return rc;
@@ -210,15 +230,23 @@ static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, u
           s.h_off[n + j] = pos + j * bs;
           s.h_len[n + j] = (uint32_t)std::min<uint64_t>(bs, f.size - off0 - j * bs);
         }
-        jobs.push_back({fi, off0, bytes, s.h_data + pos});
+        for (uint64_t piece = 0; piece < bytes; piece += kReadPiece)
+          jobs.push_back({fi, off0 + piece, std::min<uint64_t>(kReadPiece, bytes - piece),
+                          s.h_data + pos + piece});
         pos += bytes;
         n += take;
         fblk += take;
       }
+      const double t_read0 = trace_on() ? now_ms() : 0;
       rc = run_reads(jobs, files, threads);
       if (rc) return rc;
+      const double t_read1 = trace_on() ? now_ms() : 0;
       rc = slot_submit(d, s, std::max<uint64_t>(pos, 16), n);
       if (rc) return rc;
+      if (trace_on())
+        fprintf(stderr, "cir_scan batch: %.1f MiB, %zu jobs, wait %.2f ms, read %.2f ms (%.1f GB/s)\n",
+                pos / 1048576.0, jobs.size(), t_wait1 - t_wait0, t_read1 - t_read0,
+                pos / 1e6 / std::max(t_read1 - t_read0, 1e-3));
       pending_first[k] = first;
       pending_n[k] = n;
     }

@@ -69,6 +69,14 @@ for s in "$@"; do
         > gpurun_out/cfg5.json 2> gpurun_out/cfg5.err
       rm -rf /dev/shm/ciruela_bench_tree
       cat gpurun_out/cfg5.json ;;
+    cfg5sweep)
+      for t in 8 16 32; do
+        CIR_SCAN_THREADS=$t CIR_TRACE=1 step "cfg5_t$t" 600 python bench.py --workload config5 --steps 2 \
+          --tree-gib "${TREE_GIB:-8}" > gpurun_out/cfg5_t$t.json 2> gpurun_out/cfg5_t$t.err
+        cat gpurun_out/cfg5_t$t.json
+        tail -3 gpurun_out/cfg5_t$t.err
+      done
+      rm -rf /dev/shm/ciruela_bench_tree ;;
     ubench)
       step ubench 300 ./build/valu_ubench > gpurun_out/ubench.log 2>&1
       cat gpurun_out/ubench.log ;;

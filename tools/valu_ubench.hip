@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "blake2b_dev.hpp"
+#include "uniform.hpp"
 
 #define CHECK(x)                                                              \
   do {                                                                        \
@@ -263,6 +264,41 @@ __global__ __launch_bounds__(256, 4) void k_compress_clk(uint8_t* out, uint32_t 
   if (threadIdx.x == 0) {
     stamps[2 * blockIdx.x] = t1 - t0;
     stamps[2 * blockIdx.x + 1] = r1 - r0;
+  }
+}
+
+// ---- production-kernel A/B (same process, interleaved rounds) -------------
+__global__ void k_fill(uint64_t* p, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    p[i] = (i + 1) * 0x9E3779B97F4A7C15ULL ^ (i >> 7);
+}
+
+// variant 0: production (uniform.hpp); 1: + stamps (clock); 2: static priority
+// for the second half of each workgroup's waves
+template <int V>
+__global__ __launch_bounds__(256, 5) void k_prod(const uint8_t* __restrict__ data, uint64_t bs,
+                                                 uint32_t lines, uint8_t* __restrict__ out,
+                                                 uint64_t* stamps) {
+  using namespace cir::dev;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kWaves * kWaveLds];
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t blk0 = ((uint64_t)blockIdx.x * kWaves + wave) * 64u;
+  uint64_t t0 = 0, r0 = 0;
+  if constexpr (V == 1) {
+    t0 = __builtin_amdgcn_s_memtime();
+    r0 = __builtin_amdgcn_s_memrealtime();
+  }
+  if constexpr (V == 2) {
+    if (wave >= 2) __builtin_amdgcn_s_setprio(1);
+  }
+  uniform_glds_wave(data + blk0 * bs, bs, lines, out + blk0 * 32u, lds + wave * kWaveLds);
+  if constexpr (V == 1) {
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if ((threadIdx.x & 63) == 0) {
+      stamps[2 * (blockIdx.x * kWaves + wave)] = t1 - t0;
+      stamps[2 * (blockIdx.x * kWaves + wave) + 1] = r1 - r0;
+    }
   }
 }
 
@@ -608,6 +644,49 @@ int main() {
     std::sort(clk.begin(), clk.end());
     printf("compress-only clock after %d launches (%.1f ms each): median %.3f GHz (p10 %.3f, p90 %.3f)\n",
            n, ms / n, clk[g / 2], clk[g / 10], clk[9 * g / 10]);
+  }
+  {
+    // 1 M x 32 KiB, interleaved rounds: production / priority variant / compress-only
+    const uint64_t nb = 1 << 20, bs = 32768, bytes = nb * bs;
+    uint8_t *data, *o2;
+    uint64_t* st;
+    CHECK(hipMalloc(&data, bytes));
+    CHECK(hipMalloc(&o2, nb * 32));
+    CHECK(hipMalloc(&st, nb / 64 * 16));
+    hipLaunchKernelGGL(k_fill, dim3(65536), dim3(256), 0, 0, (uint64_t*)data, bytes / 8);
+    CHECK(hipDeviceSynchronize());
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    auto tp = [&](int v) {
+      (void)hipEventRecord(a);
+      if (v == 0) hipLaunchKernelGGL(k_prod<0>, dim3(nb / 256), dim3(256), 0, 0, data, bs, 256u, o2, st);
+      if (v == 1) hipLaunchKernelGGL(k_prod<1>, dim3(nb / 256), dim3(256), 0, 0, data, bs, 256u, o2, st);
+      if (v == 2) hipLaunchKernelGGL(k_prod<2>, dim3(nb / 256), dim3(256), 0, 0, data, bs, 256u, o2, st);
+      if (v == 3) hipLaunchKernelGGL(k_compress_wg<256>, dim3(nb / 256), dim3(256), 0, 0, o2, 256u);
+      (void)hipEventRecord(b);
+      (void)hipEventSynchronize(b);
+      float ms;
+      (void)hipEventElapsedTime(&ms, a, b);
+      return ms;
+    };
+    const char* names[] = {"production k_uniform_glds", "production + stamps", "production + setprio(1) waves 2-3",
+                           "compress-only (no memory)"};
+    std::vector<float> t[4];
+    for (int v = 0; v < 4; ++v) tp(v);
+    for (int round = 0; round < 7; ++round)
+      for (int v = 0; v < 4; ++v) t[v].push_back(tp(v));
+    for (int v = 0; v < 4; ++v) {
+      std::sort(t[v].begin(), t[v].end());
+      printf("AB %-36s median %.3f ms  min %.3f ms\n", names[v], t[v][3], t[v][0]);
+    }
+    std::vector<uint64_t> hs(nb / 64 * 2);
+    CHECK(hipMemcpy(hs.data(), st, hs.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<double> clk;
+    for (size_t i = 0; i < nb / 64; ++i) clk.push_back((double)hs[2 * i] / (double)hs[2 * i + 1] * 0.1);
+    std::sort(clk.begin(), clk.end());
+    printf("AB production kernel in-kernel clock: median %.3f GHz (p10 %.3f p90 %.3f)\n",
+           clk[clk.size() / 2], clk[clk.size() / 10], clk[9 * clk.size() / 10]);
   }
   CHECK(hipDeviceSynchronize());
   return 0;
