@@ -128,6 +128,61 @@ __constant__ uint8_t kSigma[12][16] = {
 
 constexpr int kQuadWaveLds = 16 * 128;  // one 128-B line per quad
 
+__device__ __forceinline__ void quad_addr(uint32_t (&addr)[48], uint32_t line, uint32_t i) {
+#pragma unroll
+  for (int r = 0; r < 12; ++r) {
+    addr[4 * r + 0] = line + 8u * kSigma[r][2 * i];
+    addr[4 * r + 1] = line + 8u * kSigma[r][2 * i + 1];
+    addr[4 * r + 2] = line + 8u * kSigma[r][8 + 2 * i];
+    addr[4 * r + 3] = line + 8u * kSigma[r][9 + 2 * i];
+  }
+}
+
+__device__ __forceinline__ uint64_t iv_lo(uint32_t i) {
+  return i == 0 ? CIR_IV0 : i == 1 ? CIR_IV1 : i == 2 ? CIR_IV2 : CIR_IV3;
+}
+__device__ __forceinline__ uint64_t iv_hi(uint32_t i) {
+  return i == 0 ? CIR_IV4 : i == 1 ? CIR_IV5 : i == 2 ? CIR_IV6 : CIR_IV7;
+}
+
+// Initial chain value of quad lane i: (h[i], h[4+i]).
+__device__ __forceinline__ void quad_init(uint32_t i, uint64_t& h0, uint64_t& h1) {
+  h0 = i == 0 ? iv_lo(0) ^ CIR_P0_256 : iv_lo(i);
+  h1 = iv_hi(i);
+}
+
+// Advance a quad's chain over L bytes at p, t0 bytes already compressed.
+// final: the last line (partial, or the empty block of an empty input)
+// carries the final flag; otherwise L must be a multiple of 128.
+__device__ __forceinline__ void quad_run(uint64_t& h0, uint64_t& h1, uint64_t t0,
+                                         const uint8_t* p, uint32_t L, bool active, bool final,
+                                         uint8_t* lds, const uint32_t (&addr)[48], uint32_t line,
+                                         uint32_t i) {
+  const uint32_t nfull = L >> 7, rem = L & 127u;
+  const uint32_t total =
+      !active ? 0u : final ? nfull + ((rem != 0u || (L == 0u && t0 == 0u)) ? 1u : 0u) : nfull;
+  const bool al16 = (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+  const uint64_t cv = iv_lo(i), dv0 = iv_hi(i);
+  auto fetch = [&](uint32_t it, uint4& u, uint4& w) {
+    const uint32_t lb = it < nfull ? 128u : rem;
+    const uint32_t n = lb > 32u * i ? min(32u, lb - 32u * i) : 0u;
+    load32_safe(u, w, p + (uint64_t)it * 128u + 32u * i, n, al16);
+  };
+  uint4 u = make_uint4(0, 0, 0, 0), w = u;
+  if (total) fetch(0, u, w);
+  for (uint32_t it = 0; it < total; ++it) {
+    // publish this lane's 32 bytes of the line to its quad (LDS is in order
+    // per wave: the previous compression's reads precede these writes)
+    *reinterpret_cast<uint4*>(lds + line + 32u * i) = u;
+    *reinterpret_cast<uint4*>(lds + line + 32u * i + 16u) = w;
+    if (it + 1 < total) fetch(it + 1, u, w);
+    const bool last = final && it + 1 == total;
+    const uint64_t t = t0 + (last ? (uint64_t)L : (uint64_t)(it + 1) * 128u);
+    const uint64_t dv = dv0 ^ (i == 0 ? t : 0ull) ^ ((i == 2 && last) ? ~0ull : 0ull);
+    compress_quad(h0, h1, lds, addr, cv, dv);
+  }
+}
+
 __device__ __forceinline__ void quad_chains(const uint8_t* __restrict__ arena,
                                             const uint64_t* __restrict__ off,
                                             const uint32_t* __restrict__ len,
@@ -147,40 +202,10 @@ __device__ __forceinline__ void quad_chains(const uint8_t* __restrict__ arena,
   const uint8_t* p = arena + o;
   const uint32_t line = wave_lds + q * 128u;  // this quad's line in LDS
   uint32_t addr[48];
-#pragma unroll
-  for (int r = 0; r < 12; ++r) {
-    addr[4 * r + 0] = line + 8u * kSigma[r][2 * i];
-    addr[4 * r + 1] = line + 8u * kSigma[r][2 * i + 1];
-    addr[4 * r + 2] = line + 8u * kSigma[r][8 + 2 * i];
-    addr[4 * r + 3] = line + 8u * kSigma[r][9 + 2 * i];
-  }
-  const uint32_t nfull = L >> 7, rem = L & 127u;
-  const uint32_t total = have ? nfull + ((rem != 0u || L == 0u) ? 1u : 0u) : 0u;
-  const bool al16 = (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
-  const uint64_t ivc[4] = {CIR_IV0, CIR_IV1, CIR_IV2, CIR_IV3};
-  const uint64_t ivd[4] = {CIR_IV4, CIR_IV5, CIR_IV6, CIR_IV7};
-  const uint64_t cv = i == 0 ? ivc[0] : i == 1 ? ivc[1] : i == 2 ? ivc[2] : ivc[3];
-  const uint64_t dv0 = i == 0 ? ivd[0] : i == 1 ? ivd[1] : i == 2 ? ivd[2] : ivd[3];
-  uint64_t h0 = i == 0 ? cv ^ CIR_P0_256 : cv;
-  uint64_t h1 = dv0;
-  auto fetch = [&](uint32_t it, uint4& u, uint4& w) {
-    const uint32_t lb = it < nfull ? 128u : rem;
-    const uint32_t n = lb > 32u * i ? min(32u, lb - 32u * i) : 0u;
-    load32_safe(u, w, p + (uint64_t)it * 128u + 32u * i, n, al16);
-  };
-  uint4 u = make_uint4(0, 0, 0, 0), w = u;
-  if (total) fetch(0, u, w);
-  for (uint32_t it = 0; it < total; ++it) {
-    // publish this lane's 32 bytes of the line to its quad (LDS is in order
-    // per wave: the previous compression's reads precede these writes)
-    *reinterpret_cast<uint4*>(lds + line + 32u * i) = u;
-    *reinterpret_cast<uint4*>(lds + line + 32u * i + 16u) = w;
-    if (it + 1 < total) fetch(it + 1, u, w);
-    const bool last = it + 1 == total;
-    const uint64_t t = last ? (uint64_t)L : (uint64_t)(it + 1) * 128u;
-    const uint64_t dv = dv0 ^ (i == 0 ? t : 0ull) ^ ((i == 2 && last) ? ~0ull : 0ull);
-    compress_quad(h0, h1, lds, addr, cv, dv);
-  }
+  quad_addr(addr, line, i);
+  uint64_t h0, h1;
+  quad_init(i, h0, h1);
+  quad_run(h0, h1, 0, p, have ? L : 0u, have, true, lds, addr, line, i);
   if (have) *reinterpret_cast<uint64_t*>(out + (uint64_t)b * 32u + 8u * i) = h0;
 }
 
@@ -206,6 +231,35 @@ __global__ __launch_bounds__(kThreads, 4) void k_mixed(const uint8_t* __restrict
   uint64_t h[8];
   hash_chain(arena + off[b], len[b], h);
   store_digest(out + (uint64_t)b * 32u, h);
+}
+
+// Resumable single chain (the index footer, fed incrementally): one quad.
+// st[0..7] = chain value, st[8] = bytes compressed so far.  After the final
+// call st[0..3] is the digest.
+__global__ __launch_bounds__(64) void k_chain_step(uint64_t* __restrict__ st,
+                                                   const uint8_t* __restrict__ data, uint32_t n,
+                                                   int final) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[128];
+  const uint32_t i = threadIdx.x;
+  if (i >= 4) return;
+  uint32_t addr[48];
+  quad_addr(addr, 0u, i);
+  const uint64_t t0 = st[8];
+  uint64_t h0 = st[i], h1 = st[4 + i];
+  if (t0 == 0 && st[9] == 0) quad_init(i, h0, h1);  // st[9] = 0: fresh state
+  quad_run(h0, h1, t0, data, n, true, final != 0, lds, addr, 0u, i);
+  st[i] = h0;
+  st[4 + i] = h1;
+  if (i == 0) {
+    st[8] = t0 + n;
+    st[9] = 1;
+  }
+}
+
+hipError_t launch_chain_step(uint64_t* st, const uint8_t* data, uint32_t n, bool final,
+                             hipStream_t s) {
+  hipLaunchKernelGGL(k_chain_step, dim3(1), dim3(64), 0, s, st, data, n, final ? 1 : 0);
+  return hipGetLastError();
 }
 
 __device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t k) {

@@ -42,6 +42,14 @@ Device::~Device() {
     if (s.copied) (void)hipEventDestroy(s.copied);
     if (s.done) (void)hipEventDestroy(s.done);
   }
+  if (chain) (void)hipStreamSynchronize(chain);
+  for (int k = 0; k < 2; ++k) {
+    (void)hipHostFree(chain_h[k]);
+    (void)hipFree(chain_d[k]);
+    if (chain_done[k]) (void)hipEventDestroy(chain_done[k]);
+  }
+  (void)hipFree(chain_state);
+  if (chain) (void)hipStreamDestroy(chain);
   if (order_free) (void)hipEventSynchronize(order_free);
   (void)hipFree(order_scratch);
   if (order_free) (void)hipEventDestroy(order_free);

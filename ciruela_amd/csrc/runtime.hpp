@@ -55,6 +55,14 @@ struct Device {
   void* order_scratch = nullptr;
   size_t order_cap = 0;
   hipEvent_t order_free = nullptr;
+  // incremental footer chain (cir_scan_v1): own stream, state, text buffers
+  std::mutex chain_mu;  // one incremental footer (scan) at a time per device
+  hipStream_t chain = nullptr;
+  uint64_t* chain_state = nullptr;  // 16 x u64
+  uint8_t* chain_h[2] = {nullptr, nullptr};
+  uint8_t* chain_d[2] = {nullptr, nullptr};
+  size_t chain_cap[2] = {0, 0};
+  hipEvent_t chain_done[2] = {nullptr, nullptr};
   ~Device();
   int ensure_slot(Slot& s, uint64_t bytes, uint64_t nblk);
 };

@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <map>
 #include <memory>
+#include <functional>
 #include <thread>
 
 #include "dirsig.hpp"
@@ -175,8 +176,10 @@ static int run_reads(const std::vector<ReadJob>& jobs, const std::vector<ScanFil
 // Batches are packed into the two staging slots of device 0 (file segments
 // 16-byte aligned, one descriptor per block) by `threads` reader threads
 // while the previous batch uploads and hashes.
+using Progress = std::function<int(uint64_t done_blk)>;
+
 static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, unsigned threads,
-                      std::vector<uint8_t>& digests) {
+                      std::vector<uint8_t>& digests, const Progress& progress) {
   uint64_t nblk_total = 0;
   for (ScanFile& f : files) {
     f.first_blk = nblk_total;
@@ -207,6 +210,8 @@ static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, u
       int rc = slot_wait(d, s);
       if (rc) return rc;
       memcpy(digests.data() + 32 * pending_first[k], s.h_out, 32 * pending_n[k]);
+      rc = progress(pending_first[k] + pending_n[k]);
+      if (rc) return rc;
     }
     const double t_wait1 = trace_on() ? now_ms() : 0;
     if (more()) {
@@ -255,6 +260,79 @@ static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, u
   return CIR_OK;
 }
 
+
+// ---- incremental footer ---------------------------------------------------
+// The footer is H(index body): one sequential chain over the whole body.  The
+// body is emitted as the files' digests come back, and every completed
+// stretch of it (whole 128-B lines, at least one byte held back for the
+// final block) is fed to a resumable single-chain kernel on the device's
+// `chain` stream, so the chain advances while later batches are still read
+// and hashed.
+struct FooterChain {
+  Device& d;
+  size_t fed = 0;
+  int k = 0;
+  explicit FooterChain(Device& dev) : d(dev) {}
+
+  int start() {
+    if (!d.chain) {
+      CIR_HIP(hipStreamCreateWithFlags(&d.chain, hipStreamNonBlocking));
+      CIR_HIP(hipMalloc(&d.chain_state, 16 * 8));
+      for (int b = 0; b < 2; ++b) CIR_HIP(hipEventCreateWithFlags(&d.chain_done[b],
+                                                                 hipEventDisableTiming));
+    }
+    CIR_HIP(hipMemsetAsync(d.chain_state, 0, 16 * 8, d.chain));
+    fed = 0;
+    return CIR_OK;
+  }
+
+  // feed body[fed, fed + n) (n whole lines unless final)
+  int push(const std::string& body, size_t n, bool final) {
+    while (n > 0 || final) {
+      const size_t piece = std::min<size_t>(n, final ? n : (size_t)256 << 20);
+      const bool last = final && piece == n;
+      CIR_HIP(hipEventSynchronize(d.chain_done[k]));  // buffer k free again
+      if (piece > d.chain_cap[k]) {
+        (void)hipHostFree(d.chain_h[k]);
+        (void)hipFree(d.chain_d[k]);
+        d.chain_h[k] = nullptr;
+        d.chain_d[k] = nullptr;
+        d.chain_cap[k] = 0;
+        const size_t cap = std::max<size_t>(piece, (size_t)4 << 20);
+        CIR_HIP(hipHostMalloc(&d.chain_h[k], cap, hipHostMallocDefault));
+        CIR_HIP(hipMalloc(&d.chain_d[k], cap));
+        d.chain_cap[k] = cap;
+      }
+      if (piece) {
+        memcpy(d.chain_h[k], body.data() + fed, piece);
+        CIR_HIP(hipMemcpyAsync(d.chain_d[k], d.chain_h[k], piece, hipMemcpyHostToDevice, d.chain));
+      }
+      CIR_HIP(dev::launch_chain_step(d.chain_state, d.chain_d[k], (uint32_t)piece, last, d.chain));
+      CIR_HIP(hipEventRecord(d.chain_done[k], d.chain));
+      k ^= 1;
+      fed += piece;
+      n -= piece;
+      if (last) break;
+    }
+    return CIR_OK;
+  }
+
+  // feed what is complete, keeping >= 1 byte back; skip tiny feeds
+  int advance(const std::string& body, size_t min_feed) {
+    const size_t avail = body.size() - fed;
+    const size_t n = avail > 0 ? (avail - 1) / 128 * 128 : 0;
+    if (n < min_feed) return CIR_OK;
+    return push(body, n, false);
+  }
+
+  int finish(const std::string& body, uint8_t out[32]) {
+    int rc = push(body, body.size() - fed, true);
+    if (rc) return rc;
+    CIR_HIP(hipMemcpyAsync(out, d.chain_state, 32, hipMemcpyDeviceToHost, d.chain));
+    CIR_HIP(hipStreamSynchronize(d.chain));
+    return CIR_OK;
+  }
+};
 
 // ---- RawIndex::into_mut + MutableIndex::to_raw_data ---------------------
 // (src/cluster/download.rs:171-188 fill_dirs :108-168, emit :266-319)
@@ -327,36 +405,42 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
     int rc = walk(dirs[i], pre, plan, files);
     if (rc) return rc;
   }
-  std::vector<uint8_t> digests;
-  int rc = hash_files(ctx, files, block_size, threads, digests);
-  if (rc) return rc;
-
   dirsig::Emitter em(hdr);
-  for (const PlanItem& it : plan) {
-    switch (it.kind) {
-      case dirsig::EntryKind::kDir:
+  Device& dv = *ctx->devs[0];
+  std::lock_guard<std::mutex> chain_lock(dv.chain_mu);
+  CIR_HIP(hipSetDevice(dv.id));
+  FooterChain chain(dv);
+  int rc = chain.start();
+  if (rc) return rc;
+  std::vector<uint8_t> digests;
+  size_t plan_pos = 0;
+  // emit every plan item whose file blocks are all hashed (files complete in
+  // plan order), then feed the finished stretch of the body to the chain
+  auto emit_ready = [&](uint64_t done_blk) -> int {
+    for (; plan_pos < plan.size(); ++plan_pos) {
+      const PlanItem& it = plan[plan_pos];
+      if (it.kind == dirsig::EntryKind::kDir) {
         em.start_dir(it.name);
-        break;
-      case dirsig::EntryKind::kFile: {
-        const ScanFile& f = files[it.file];
-        em.add_file(it.name, it.exe, f.size, digests.data() + 32 * f.first_blk,
-                    (f.size + block_size - 1) / block_size);
-        break;
-      }
-      case dirsig::EntryKind::kLink:
+      } else if (it.kind == dirsig::EntryKind::kLink) {
         em.add_symlink(it.name, it.target);
-        break;
+      } else {
+        const ScanFile& f = files[it.file];
+        const uint64_t nb = (f.size + block_size - 1) / block_size;
+        if (f.first_blk + nb > done_blk) break;
+        em.add_file(it.name, it.exe, f.size, digests.data() + 32 * f.first_blk, nb);
+      }
     }
-  }
-  // Footer = H(every byte after the header line), hashed on the GPU.
+    return chain.advance(em.body(), (size_t)1 << 20);
+  };
+  rc = hash_files(ctx, files, block_size, threads, digests, emit_ready);
+  if (rc) return rc;
+  rc = emit_ready(~0ull);
+  if (rc) return rc;
+  // Footer = H(every byte after the header line), finished on the GPU.
   const std::string& body = em.body();
-  if (body.size() > 0xffffffffull) return fail(CIR_EINVAL, "index body longer than 4 GiB");
+  if (body.size() - chain.fed > 0xffffffffull) return fail(CIR_EINVAL, "index tail above 4 GiB");
   uint8_t footer[32];
-  const uint64_t off = 0;
-  const uint32_t len = (uint32_t)body.size();
-  static const uint8_t empty = 0;
-  rc = cir_hash_blocks(ctx, body.empty() ? &empty : (const uint8_t*)body.data(), &off, &len, 1,
-                       footer);
+  rc = chain.finish(body, footer);
   if (rc) return rc;
   const std::string out = em.finish(footer, 32);
   *index_out = (uint8_t*)malloc(out.size());

@@ -77,6 +77,11 @@ for s in "$@"; do
         tail -3 gpurun_out/cfg5_t$t.err
       done
       rm -rf /dev/shm/ciruela_bench_tree ;;
+    dist1)
+      step dist1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+        --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 1 --steps 5 --warmup 1 --force-dist \
+        --no-cpu-baseline > gpurun_out/dist1.json 2> gpurun_out/dist1.err
+      cat gpurun_out/dist1.json ;;
     ubench)
       step ubench 300 ./build/valu_ubench > gpurun_out/ubench.log 2>&1
       cat gpurun_out/ubench.log ;;
