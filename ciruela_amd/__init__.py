@@ -32,7 +32,7 @@ from ._native import CiruelaError, NoDevice  # noqa: F401
 __all__ = [
     "BlockHash", "ImageId", "HashType", "Hashes", "ScannerConfig", "v1", "get_hash",
     "InMemoryIndexes", "ThreadedBlockReader", "BlockHint", "Context", "default_context",
-    "IndexError_", "DirError", "ReadError", "CiruelaError", "NoDevice",
+    "IndexError_", "DirError", "ReadError", "CiruelaError", "NoDevice", "sha512_256",
 ]
 
 DEFAULT_BLOCK_SIZE = 32768
@@ -85,12 +85,15 @@ class Context:
     def hash_chunks_dev(self, d_data, nbytes, block_size, d_out, stream=0):
         _n.check(_n.lib.cir_hash_chunks_dev(self._h, d_data, nbytes, block_size, d_out, stream))
 
-    def hash_blocks_dev(self, d_arena, d_off, d_len, nblk, d_out, stream=0):
-        _n.check(_n.lib.cir_hash_blocks_dev(self._h, d_arena, d_off, d_len, nblk, d_out, stream))
+    def hash_blocks_dev(self, d_arena, d_off, d_len, nblk, d_out, stream=0, hash_type=None):
+        ht = (hash_type or HashType.blake2b_256()).code
+        _n.check(_n.lib.cir_hash_blocks_dev_ht(self._h, ht, d_arena, d_off, d_len, nblk, d_out,
+                                               stream))
 
     # ---- host-memory entry points ----------------------------------------
-    def hash_blocks(self, arena, offsets, lengths):
+    def hash_blocks(self, arena, offsets, lengths, hash_type=None):
         """Digests (n x 32 bytes) of arena[off[i] : off[i] + len[i]]."""
+        ht = (hash_type or HashType.blake2b_256()).code
         n = len(offsets)
         if len(lengths) != n:
             raise ValueError("offsets and lengths differ in length")
@@ -106,26 +109,70 @@ class Context:
         if ptr is None:
             one = ctypes.create_string_buffer(1)
             ptr, keep = ctypes.cast(one, ctypes.c_void_p), one
-        _n.check(_n.lib.cir_hash_blocks(self._h, ptr, offs, lens, n, out))
+        _n.check(_n.lib.cir_hash_blocks_ht(self._h, ht, ptr, offs, lens, n, out))
         del keep
         return out.raw[:32 * n]
 
-    def hash_file(self, fd, block_size):
+    def hash_file(self, fd, block_size, hash_type=None):
+        ht = (hash_type or HashType.blake2b_256()).code
         size = ctypes.c_uint64()
         hp = ctypes.c_void_p()
         nh = ctypes.c_size_t()
-        _n.check(_n.lib.cir_hash_file(self._h, fd, block_size, ctypes.byref(size),
-                                      ctypes.byref(hp), ctypes.byref(nh)))
+        _n.check(_n.lib.cir_hash_file_ht(self._h, ht, fd, block_size, ctypes.byref(size),
+                                         ctypes.byref(hp), ctypes.byref(nh)))
         return size.value, _n.take_buffer(hp.value, 32 * nh.value)
 
-    def hash_memory(self, data, block_size):
+    def hash_memory(self, data, block_size, hash_type=None):
+        ht = (hash_type or HashType.blake2b_256()).code
         ptr, keep = _buf(data)
         hp = ctypes.c_void_p()
         nh = ctypes.c_size_t()
-        _n.check(_n.lib.cir_hash_memory(self._h, ptr, len(data), block_size, ctypes.byref(hp),
-                                        ctypes.byref(nh)))
+        _n.check(_n.lib.cir_hash_memory_ht(self._h, ht, ptr, len(data), block_size,
+                                           ctypes.byref(hp), ctypes.byref(nh)))
         del keep
         return _n.take_buffer(hp.value, 32 * nh.value)
+
+    # ---- verification (daemon side, fetch_blocks.rs:77 / commit.rs:104) --
+    def verify_blocks(self, arena, offsets, lengths, expected, hash_type=None):
+        """Per block: does H(arena[off:off+len]) equal expected[32 i:32 i+32]?"""
+        ht = (hash_type or HashType.blake2b_256()).code
+        n = len(offsets)
+        if len(lengths) != n or len(expected) != 32 * n:
+            raise ValueError("offsets, lengths and expected digests disagree in length")
+        for o, ln in zip(offsets, lengths):
+            if o < 0 or ln < 0 or o + ln > len(arena):
+                raise ValueError("block outside the arena")
+        if n == 0:
+            return []
+        offs = (ctypes.c_uint64 * n)(*offsets)
+        lens = (ctypes.c_uint32 * n)(*lengths)
+        ptr, keep = _buf(arena) if len(arena) else (None, None)
+        if ptr is None:
+            one = ctypes.create_string_buffer(1)
+            ptr, keep = ctypes.cast(one, ctypes.c_void_p), one
+        exp = ctypes.create_string_buffer(bytes(expected), 32 * n)
+        ok = ctypes.create_string_buffer(n)
+        nbad = ctypes.c_size_t()
+        _n.check(_n.lib.cir_verify_blocks(self._h, ht, ptr, offs, lens, n, exp, ok,
+                                          ctypes.byref(nbad)))
+        del keep
+        return [b == 1 for b in ok.raw]
+
+    def verify_blocks_dev(self, d_arena, d_off, d_len, nblk, d_expected, d_digests, d_ok=0,
+                          d_nbad=0, stream=0, hash_type=None):
+        ht = (hash_type or HashType.blake2b_256()).code
+        _n.check(_n.lib.cir_verify_blocks_dev(self._h, ht, d_arena, d_off, d_len, nblk,
+                                              d_expected, d_digests, d_ok, d_nbad, stream))
+
+    def check_file(self, fd, block_size, expected, hash_type=None):
+        ht = (hash_type or HashType.blake2b_256()).code
+        if len(expected) % 32:
+            raise ValueError("expected digests must be 32 bytes each")
+        n = len(expected) // 32
+        exp = ctypes.create_string_buffer(bytes(expected), max(len(expected), 1))
+        ok = ctypes.c_int()
+        _n.check(_n.lib.cir_check_file(self._h, ht, fd, block_size, exp, n, ctypes.byref(ok)))
+        return ok.value == 1
 
     def scan(self, config):
         dirs = [os.fsencode(d) for d, _ in config._dirs]
@@ -275,14 +322,12 @@ class Hashes:
 
         reader: an int fd, an object with fileno(), or bytes-like data.
         """
-        if hash_type.code != _n.CIR_HASH_BLAKE2B_256:
-            raise CiruelaError(_n.CIR_EUNSUPPORTED, "only blake2b/256 runs on the GPU")
         ctx = context or default_context()
         if isinstance(reader, (bytes, bytearray, memoryview)):
-            raw = ctx.hash_memory(reader, block_size)
+            raw = ctx.hash_memory(reader, block_size, hash_type)
             return len(reader), Hashes(raw, block_size, hash_type)
         fd = reader if isinstance(reader, int) else reader.fileno()
-        size, raw = ctx.hash_file(fd, block_size)
+        size, raw = ctx.hash_file(fd, block_size, hash_type)
         return size, Hashes(raw, block_size, hash_type)
 
     def __len__(self):
@@ -299,6 +344,13 @@ class Hashes:
 
     def raw(self):
         return self._raw
+
+    def check_file(self, reader, context=None):
+        """Hashes::check_file (src/daemon/disk/commit.rs:104): re-hash the file
+        on the GPU; True iff it has exactly these blocks."""
+        ctx = context or default_context()
+        fd = reader if isinstance(reader, int) else reader.fileno()
+        return ctx.check_file(fd, self._bs, self._raw, self._ht)
 
 
 class ScannerConfig:
@@ -350,6 +402,15 @@ class v1:  # noqa: N801 - mirrors the `dir_signature::v1` module
         if out is not None:
             out.extend(data)
         return data
+
+
+def sha512_256(data):
+    """SHA-512/256 of data on the GPU (dir-signature's HashType::sha512_256)."""
+    ptr, keep = _buf(bytes(data)) if len(data) else (None, None)
+    out = ctypes.create_string_buffer(32)
+    _n.check(_n.lib.cir_sha512_256(ptr, len(data), out))
+    del keep
+    return out.raw
 
 
 def get_hash(index):
@@ -452,7 +513,8 @@ class ThreadedBlockReader:
 
     def register_memory_blocks(self, hash_type, block_size, data, context=None):
         if hash_type.code != _n.CIR_HASH_BLAKE2B_256:
-            raise CiruelaError(_n.CIR_EUNSUPPORTED, "only blake2b/256 runs on the GPU")
+            # BlockHash (src/block_id.rs:37-43) is BLAKE2b-256 only
+            raise CiruelaError(_n.CIR_EUNSUPPORTED, "block ids are blake2b/256")
         ctx = context or default_context()
         ptr, keep = _buf(bytes(data)) if len(data) else (None, None)
         _n.check(_n.lib.cir_blocks_register_memory(ctx.handle, self._h, ptr, len(data),

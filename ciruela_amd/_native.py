@@ -83,6 +83,21 @@ _SIGS = {
     "cir_blocks_register_memory": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_size_t,
                                                   ctypes.c_uint64]),
     "cir_blocks_read": (ctypes.c_int, [c_vp, c_vp, ctypes.POINTER(c_vp), c_sizep]),
+    "cir_sha512_256": (ctypes.c_int, [c_vp, ctypes.c_size_t, c_vp]),
+    "cir_hash_blocks_dev_ht": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, c_vp, c_vp, ctypes.c_size_t,
+                                              c_vp, c_vp]),
+    "cir_hash_blocks_ht": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, c_vp, c_vp, ctypes.c_size_t,
+                                          c_vp]),
+    "cir_hash_file_ht": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, c_u64p,
+                                        ctypes.POINTER(c_vp), c_sizep]),
+    "cir_hash_memory_ht": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, ctypes.c_uint64,
+                                          ctypes.c_uint64, ctypes.POINTER(c_vp), c_sizep]),
+    "cir_verify_blocks_dev": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, c_vp, c_vp, ctypes.c_size_t,
+                                             c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "cir_verify_blocks": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, c_vp, c_vp, ctypes.c_size_t,
+                                         c_vp, c_vp, c_sizep]),
+    "cir_check_file": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, c_vp,
+                                      ctypes.c_size_t, ctypes.POINTER(ctypes.c_int)]),
     "cir_debug_hash_uniform_dev": (ctypes.c_int, [ctypes.c_int, c_vp, ctypes.c_uint64,
                                                   ctypes.c_uint64, c_vp, c_vp]),
     "cir_fill_splitmix64_dev": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint64,

@@ -18,9 +18,12 @@
 
 #include "blake2b_dev.hpp"
 #include "uniform.hpp"
+#include "sha512_dev.hpp"
 
 namespace cir {
 namespace dev {
+
+static inline unsigned grid_for(uint64_t n, uint64_t per) { return (unsigned)((n + per - 1) / per); }
 
 // Pure uniform launch: nblk = gridDim.x * 256 equal blocks.
 __global__ __launch_bounds__(kThreads, 5) void k_uniform_glds(const uint8_t* __restrict__ data,
@@ -262,6 +265,56 @@ hipError_t launch_chain_step(uint64_t* st, const uint8_t* data, uint32_t n, bool
   return hipGetLastError();
 }
 
+// SHA-512/256 over a descriptor batch, one lane per block (dir-signature's
+// HashType::sha512_256()).
+__global__ __launch_bounds__(kThreads, 2) void k_sha_desc(const uint8_t* __restrict__ arena,
+                                                           const uint64_t* __restrict__ off,
+                                                           const uint32_t* __restrict__ len,
+                                                           const uint32_t* __restrict__ perm,
+                                                           uint64_t n, uint8_t* __restrict__ out) {
+  const uint64_t j = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (j >= n) return;
+  const uint64_t b = perm ? perm[j] : j;
+  uint64_t h[8];
+  sha::chain(arena + off[b], len[b], h);
+  sha::store_digest_be(out + b * 32u, h);
+}
+
+hipError_t launch_sha_desc(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
+                           const uint32_t* perm, uint64_t n, uint8_t* out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sha_desc, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, arena, off,
+                     len, perm, n, out);
+  return hipGetLastError();
+}
+
+// Daemon-side verify (fetch_blocks.rs:77 `hash_bytes(&data) == blk.hash`):
+// one lane per digest, mismatches counted per wave with a ballot.
+__global__ void k_verify(const uint8_t* __restrict__ got, const uint8_t* __restrict__ want,
+                         uint64_t n, uint8_t* __restrict__ ok, uint32_t* __restrict__ nbad) {
+  const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool bad = false;
+  if (b < n) {
+    const uint4* g = reinterpret_cast<const uint4*>(got + 32 * b);
+    const uint4* w = reinterpret_cast<const uint4*>(want + 32 * b);
+    const uint4 g0 = g[0], g1 = g[1], w0 = w[0], w1 = w[1];
+    const uint32_t diff = (g0.x ^ w0.x) | (g0.y ^ w0.y) | (g0.z ^ w0.z) | (g0.w ^ w0.w) |
+                          (g1.x ^ w1.x) | (g1.y ^ w1.y) | (g1.z ^ w1.z) | (g1.w ^ w1.w);
+    bad = diff != 0;
+    if (ok) ok[b] = bad ? 0 : 1;
+  }
+  const uint64_t mask = __ballot(bad);
+  if (nbad && (threadIdx.x & 63) == 0 && mask) atomicAdd(nbad, (uint32_t)__popcll(mask));
+}
+
+hipError_t launch_verify(const uint8_t* got, const uint8_t* want, uint64_t n, uint8_t* ok,
+                         uint32_t* nbad, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_verify, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, got, want, n,
+                     ok, nbad);
+  return hipGetLastError();
+}
+
 __device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t k) {
   uint64_t z = seed + (k + 1) * 0x9e3779b97f4a7c15ULL;
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
@@ -286,7 +339,6 @@ __global__ void k_fill_splitmix64(uint64_t* __restrict__ p, uint64_t nwords, uin
   }
 }
 
-static inline unsigned grid_for(uint64_t n, uint64_t per) { return (unsigned)((n + per - 1) / per); }
 
 hipError_t launch_uniform(Loader loader, const uint8_t* data, uint64_t bs, uint64_t nblk,
                           uint8_t* out, hipStream_t s) {

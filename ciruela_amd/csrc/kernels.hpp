@@ -47,12 +47,21 @@ size_t order_scratch_bytes(uint64_t n);
 hipError_t launch_order_desc(const uint32_t* len, uint64_t n, void* scratch, size_t bytes,
                              uint32_t** perm, uint32_t** n_long, hipStream_t s);
 
+// SHA-512/256 per descriptor (one lane per block), digest b -> out + 32 b.
+hipError_t launch_sha_desc(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
+                           const uint32_t* perm, uint64_t n, uint8_t* out, hipStream_t s);
+
 // Resumable single-chain BLAKE2b-256 (quad mode).  st: 16 x u64 of device
 // memory, zeroed before the first call.  Non-final calls take a multiple of
 // 128 bytes; the final call takes the rest (>= 1 byte unless the whole input
 // is empty) and leaves the digest in st[0..3].
 hipError_t launch_chain_step(uint64_t* st, const uint8_t* data, uint32_t n, bool final,
                              hipStream_t s);
+
+// Compare n digests (32 B each, both 16-B aligned) with the expected ones:
+// ok[b] = 1 / 0 (ok may be null); *nbad += mismatches (nbad may be null).
+hipError_t launch_verify(const uint8_t* got, const uint8_t* want, uint64_t n, uint8_t* ok,
+                         uint32_t* nbad, hipStream_t s);
 
 hipError_t launch_fill_splitmix64(uint64_t* p, uint64_t nwords, uint64_t seed,
                                   uint64_t block_words, uint64_t first_block, hipStream_t s);

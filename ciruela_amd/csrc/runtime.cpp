@@ -99,8 +99,10 @@ int Device::ensure_slot(Slot& s, uint64_t bytes, uint64_t nblk) {
 
 // Descriptor batch, longest chain first: device sort (order.hip) into the
 // device's ordering scratch, then the general kernel through the permutation.
+bool valid_hash_type(int ht) { return ht == CIR_HASH_BLAKE2B_256 || ht == CIR_HASH_SHA512_256; }
+
 int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, const uint32_t* len,
-                      uint64_t n, uint8_t* out, hipStream_t s) {
+                      uint64_t n, uint8_t* out, hipStream_t s, int ht) {
   // Every batch is ordered (even a single chain: an index footer is one long
   // chain and runs in quad mode).
   if (n == 0) return CIR_OK;
@@ -119,7 +121,10 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
   uint32_t* perm = nullptr;
   uint32_t* n_long = nullptr;
   CIR_HIP(dev::launch_order_desc(len, n, d.order_scratch, d.order_cap, &perm, &n_long, s));
-  CIR_HIP(dev::launch_mixed(arena, off, len, perm, n_long, n, out, s));
+  if (ht == CIR_HASH_SHA512_256)
+    CIR_HIP(dev::launch_sha_desc(arena, off, len, perm, n, out, s));
+  else
+    CIR_HIP(dev::launch_mixed(arena, off, len, perm, n_long, n, out, s));
   CIR_HIP(hipEventRecord(d.order_free, s));
   return CIR_OK;
 }
@@ -128,7 +133,7 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
 // (h_off/h_len, nblk blocks); otherwise the slot holds `bytes` consecutive
 // bytes of one file split into chunk_bs blocks (nblk = ceil(bytes / bs)).
 static int slot_submit_impl(Device& d, Slot& s, uint64_t bytes, uint64_t nblk,
-                            uint64_t chunk_bs) {
+                            uint64_t chunk_bs, int ht) {
   CIR_HIP(hipMemcpyAsync(s.d_data, s.h_data, bytes, hipMemcpyHostToDevice, d.copy));
   if (chunk_bs == 0) {
     CIR_HIP(hipMemcpyAsync(s.d_off, s.h_off, nblk * 8, hipMemcpyHostToDevice, d.copy));
@@ -137,7 +142,7 @@ static int slot_submit_impl(Device& d, Slot& s, uint64_t bytes, uint64_t nblk,
   CIR_HIP(hipEventRecord(s.copied, d.copy));
   CIR_HIP(hipStreamWaitEvent(d.compute, s.copied, 0));
   if (chunk_bs == 0) {
-    int rc = hash_desc_ordered(d, s.d_data, s.d_off, s.d_len, nblk, s.d_out, d.compute);
+    int rc = hash_desc_ordered(d, s.d_data, s.d_off, s.d_len, nblk, s.d_out, d.compute, ht);
     if (rc) return rc;
   } else
     CIR_HIP(dev::launch_chunks(s.d_data, bytes, chunk_bs, s.d_out, d.compute));
@@ -147,8 +152,8 @@ static int slot_submit_impl(Device& d, Slot& s, uint64_t bytes, uint64_t nblk,
   return CIR_OK;
 }
 
-int slot_submit(Device& d, Slot& s, uint64_t bytes, uint64_t nblk) {
-  return slot_submit_impl(d, s, bytes, nblk, 0);
+int slot_submit(Device& d, Slot& s, uint64_t bytes, uint64_t nblk, int ht) {
+  return slot_submit_impl(d, s, bytes, nblk, 0, ht);
 }
 
 int slot_wait(Device& d, Slot& s) {
@@ -173,7 +178,7 @@ static int check_device(int id) {
 // Hash blocks [b0, b1) of a host arena on device d, packing them 16-byte
 // aligned into the two staging slots (pack slot k+1 while slot k hashes).
 static int run_blocks(cir_ctx* ctx, Device& d, const uint8_t* arena, const uint64_t* off,
-                      const uint32_t* len, size_t b0, size_t b1, uint8_t* out) {
+                      const uint32_t* len, size_t b0, size_t b1, uint8_t* out, int ht) {
   std::lock_guard<std::mutex> lk(d.mu);
   CIR_HIP(hipSetDevice(d.id));
   const uint64_t cap = ctx->staging;
@@ -209,7 +214,7 @@ static int run_blocks(cir_ctx* ctx, Device& d, const uint8_t* arena, const uint6
         memcpy(s.h_data + pos, arena + off[next + i], len[next + i]);
         pos += len[next + i];
       }
-      rc = slot_submit(d, s, std::max<uint64_t>(pos, 1), n);
+      rc = slot_submit(d, s, std::max<uint64_t>(pos, 1), n, ht);
       if (rc) return rc;
       pending_first[k] = next;
       pending_n[k] = n;
@@ -246,7 +251,7 @@ static int for_each_device(cir_ctx* ctx, const std::function<int(cir::Device&, s
 using Reader = std::function<int64_t(uint8_t*, uint64_t)>;
 
 static int run_file(cir_ctx* ctx, const Reader& rd, uint64_t bs, uint64_t* size_out,
-                    std::vector<uint8_t>& hashes) {
+                    std::vector<uint8_t>& hashes, int ht) {
   Device& d = *ctx->devs[0];
   std::lock_guard<std::mutex> lk(d.mu);
   CIR_HIP(hipSetDevice(d.id));
@@ -283,7 +288,15 @@ static int run_file(cir_ctx* ctx, const Reader& rd, uint64_t bs, uint64_t* size_
         pending_at[k] = hashes.size() / 32;
         pending_n[k] = n;
         hashes.resize(hashes.size() + 32 * n);
-        rc = slot_submit_impl(d, s, got, n, bs);
+        if (ht == CIR_HASH_BLAKE2B_256) {
+          rc = slot_submit_impl(d, s, got, n, bs, ht);
+        } else {  // descriptor form: one descriptor per block of the chunk
+          for (uint64_t b = 0; b < n; ++b) {
+            s.h_off[b] = b * bs;
+            s.h_len[b] = (uint32_t)std::min<uint64_t>(bs, got - b * bs);
+          }
+          rc = slot_submit_impl(d, s, got, n, 0, ht);
+        }
         if (rc) return rc;
         total += got;
       }
@@ -397,15 +410,17 @@ int cir_hash_chunks_dev(cir_ctx* ctx, const void* d_data, uint64_t nbytes, uint6
   return CIR_OK;
 }
 
-int cir_hash_blocks_dev(cir_ctx* ctx, const void* d_arena, const uint64_t* d_off,
-                        const uint32_t* d_len, size_t nblk, uint8_t* d_out, void* stream) {
+int cir_hash_blocks_dev_ht(cir_ctx* ctx, int hash_type, const void* d_arena,
+                           const uint64_t* d_off, const uint32_t* d_len, size_t nblk,
+                           uint8_t* d_out, void* stream) {
+  if (!valid_hash_type(hash_type)) return fail(CIR_EINVAL, "unknown hash type");
   if (nblk && (!d_arena || !d_off || !d_len || !d_out))
     return fail(CIR_EINVAL, "null device pointer");
   if (nblk > 0xffffffffull) return fail(CIR_EINVAL, "more than 2^32 descriptors");
   hipStream_t s = (hipStream_t)stream;
   // Context-less calls hash in descriptor order, one lane per chain; with a
   // context the batch is ordered longest chain first on the device
-  // (order.hip) and long chains run in quad mode.
+  // (order.hip) and long BLAKE2b chains run in quad mode.
   if (ctx) {
     int id = 0;
     if (s)
@@ -416,15 +431,25 @@ int cir_hash_blocks_dev(cir_ctx* ctx, const void* d_arena, const uint64_t* d_off
     for (auto& p : ctx->devs)
       if (p->id == id) d = p.get();
     if (!d) return fail(CIR_EINVAL, "stream device is not part of the context");
-    return hash_desc_ordered(*d, (const uint8_t*)d_arena, d_off, d_len, nblk, d_out, s);
+    return hash_desc_ordered(*d, (const uint8_t*)d_arena, d_off, d_len, nblk, d_out, s, hash_type);
   }
-  CIR_HIP(dev::launch_general_desc((const uint8_t*)d_arena, d_off, d_len, nullptr, nblk, d_out, s));
+  if (hash_type == CIR_HASH_SHA512_256)
+    CIR_HIP(dev::launch_sha_desc((const uint8_t*)d_arena, d_off, d_len, nullptr, nblk, d_out, s));
+  else
+    CIR_HIP(dev::launch_general_desc((const uint8_t*)d_arena, d_off, d_len, nullptr, nblk, d_out, s));
   return CIR_OK;
 }
 
-int cir_hash_blocks(cir_ctx* ctx, const uint8_t* h_arena, const uint64_t* off,
-                    const uint32_t* len, size_t nblk, uint8_t* h_out) {
+int cir_hash_blocks_dev(cir_ctx* ctx, const void* d_arena, const uint64_t* d_off,
+                        const uint32_t* d_len, size_t nblk, uint8_t* d_out, void* stream) {
+  return cir_hash_blocks_dev_ht(ctx, CIR_HASH_BLAKE2B_256, d_arena, d_off, d_len, nblk, d_out,
+                                stream);
+}
+
+int cir_hash_blocks_ht(cir_ctx* ctx, int hash_type, const uint8_t* h_arena, const uint64_t* off,
+                       const uint32_t* len, size_t nblk, uint8_t* h_out) {
   if (!ctx) return fail(CIR_EINVAL, "null ctx");
+  if (!valid_hash_type(hash_type)) return fail(CIR_EINVAL, "unknown hash type");
   if (nblk == 0) return CIR_OK;
   if (!h_arena || !off || !len || !h_out) return fail(CIR_EINVAL, "null pointer");
   // contiguous ranges balanced by bytes
@@ -441,11 +466,16 @@ int cir_hash_blocks(cir_ctx* ctx, const uint8_t* h_arena, const uint64_t* off,
   }
   return for_each_device(ctx, [&](Device& d, size_t i) {
     if (i >= nd || cut[i] >= cut[i + 1]) return (int)CIR_OK;
-    return run_blocks(ctx, d, h_arena, off, len, cut[i], cut[i + 1], h_out);
+    return run_blocks(ctx, d, h_arena, off, len, cut[i], cut[i + 1], h_out, hash_type);
   });
 }
 
-int cir_blake2b256(const uint8_t* p, size_t n, uint8_t out[CIR_DIGEST_BYTES]) {
+int cir_hash_blocks(cir_ctx* ctx, const uint8_t* h_arena, const uint64_t* off,
+                    const uint32_t* len, size_t nblk, uint8_t* h_out) {
+  return cir_hash_blocks_ht(ctx, CIR_HASH_BLAKE2B_256, h_arena, off, len, nblk, h_out);
+}
+
+static int single_shot(int ht, const uint8_t* p, size_t n, uint8_t* out) {
   if (!out || (n && !p)) return fail(CIR_EINVAL, "null pointer");
   if (n > 0xffffffffull) return fail(CIR_EINVAL, "block longer than 4 GiB");
   cir_ctx* ctx = nullptr;
@@ -454,13 +484,23 @@ int cir_blake2b256(const uint8_t* p, size_t n, uint8_t out[CIR_DIGEST_BYTES]) {
   static const uint8_t empty = 0;
   const uint64_t off = 0;
   const uint32_t len = (uint32_t)n;
-  return cir_hash_blocks(ctx, n ? p : &empty, &off, &len, 1, out);
+  return cir_hash_blocks_ht(ctx, ht, n ? p : &empty, &off, &len, 1, out);
 }
 
-int cir_hash_file(cir_ctx* ctx, int fd, uint64_t block_size, uint64_t* size_out,
-                  uint8_t** hashes_out, size_t* nhash_out) {
+int cir_blake2b256(const uint8_t* p, size_t n, uint8_t out[CIR_DIGEST_BYTES]) {
+  return single_shot(CIR_HASH_BLAKE2B_256, p, n, out);
+}
+
+int cir_sha512_256(const uint8_t* p, size_t n, uint8_t out[CIR_DIGEST_BYTES]) {
+  return single_shot(CIR_HASH_SHA512_256, p, n, out);
+}
+
+int cir_hash_file_ht(cir_ctx* ctx, int hash_type, int fd, uint64_t block_size,
+                     uint64_t* size_out, uint8_t** hashes_out, size_t* nhash_out) {
   if (!ctx || !size_out || !hashes_out || !nhash_out) return fail(CIR_EINVAL, "null pointer");
-  if (block_size == 0) return fail(CIR_EINVAL, "block_size must be > 0");
+  if (block_size == 0 || block_size > 0xffffffffull)
+    return fail(CIR_EINVAL, "block_size must be in 1 .. 2^32-1");
+  if (!valid_hash_type(hash_type)) return fail(CIR_EINVAL, "unknown hash type");
   std::vector<uint8_t> h;
   Reader rd = [fd](uint8_t* dst, uint64_t n) -> int64_t {
     for (;;) {
@@ -469,15 +509,23 @@ int cir_hash_file(cir_ctx* ctx, int fd, uint64_t block_size, uint64_t* size_out,
       return r < 0 ? -(int64_t)errno : (int64_t)r;
     }
   };
-  int rc = run_file(ctx, rd, block_size, size_out, h);
+  int rc = run_file(ctx, rd, block_size, size_out, h, hash_type);
   if (rc) return rc;
   return export_hashes(h, hashes_out, nhash_out);
 }
 
-int cir_hash_memory(cir_ctx* ctx, const uint8_t* data, uint64_t size, uint64_t block_size,
-                    uint8_t** hashes_out, size_t* nhash_out) {
+int cir_hash_file(cir_ctx* ctx, int fd, uint64_t block_size, uint64_t* size_out,
+                  uint8_t** hashes_out, size_t* nhash_out) {
+  return cir_hash_file_ht(ctx, CIR_HASH_BLAKE2B_256, fd, block_size, size_out, hashes_out,
+                          nhash_out);
+}
+
+int cir_hash_memory_ht(cir_ctx* ctx, int hash_type, const uint8_t* data, uint64_t size,
+                       uint64_t block_size, uint8_t** hashes_out, size_t* nhash_out) {
   if (!ctx || !hashes_out || !nhash_out || (size && !data)) return fail(CIR_EINVAL, "null pointer");
-  if (block_size == 0) return fail(CIR_EINVAL, "block_size must be > 0");
+  if (block_size == 0 || block_size > 0xffffffffull)
+    return fail(CIR_EINVAL, "block_size must be in 1 .. 2^32-1");
+  if (!valid_hash_type(hash_type)) return fail(CIR_EINVAL, "unknown hash type");
   uint64_t pos = 0, got_size = 0;
   Reader rd = [&](uint8_t* dst, uint64_t n) -> int64_t {
     const uint64_t k = std::min(n, size - pos);
@@ -486,9 +534,61 @@ int cir_hash_memory(cir_ctx* ctx, const uint8_t* data, uint64_t size, uint64_t b
     return (int64_t)k;
   };
   std::vector<uint8_t> h;
-  int rc = run_file(ctx, rd, block_size, &got_size, h);
+  int rc = run_file(ctx, rd, block_size, &got_size, h, hash_type);
   if (rc) return rc;
   return export_hashes(h, hashes_out, nhash_out);
+}
+
+int cir_hash_memory(cir_ctx* ctx, const uint8_t* data, uint64_t size, uint64_t block_size,
+                    uint8_t** hashes_out, size_t* nhash_out) {
+  return cir_hash_memory_ht(ctx, CIR_HASH_BLAKE2B_256, data, size, block_size, hashes_out,
+                            nhash_out);
+}
+
+// ---- verification (row f2) ---------------------------------------------
+
+int cir_verify_blocks_dev(cir_ctx* ctx, int hash_type, const void* d_arena, const uint64_t* d_off,
+                          const uint32_t* d_len, size_t nblk, const uint8_t* d_expected,
+                          uint8_t* d_digests, uint8_t* d_ok, uint32_t* d_nbad, void* stream) {
+  if (nblk && (!d_expected || !d_digests)) return fail(CIR_EINVAL, "null device pointer");
+  if ((reinterpret_cast<uintptr_t>(d_expected) | reinterpret_cast<uintptr_t>(d_digests)) & 15u)
+    return fail(CIR_EINVAL, "digest arrays must be 16-byte aligned");
+  hipStream_t s = (hipStream_t)stream;
+  if (d_nbad) CIR_HIP(hipMemsetAsync(d_nbad, 0, 4, s));
+  int rc = cir_hash_blocks_dev_ht(ctx, hash_type, d_arena, d_off, d_len, nblk, d_digests, stream);
+  if (rc) return rc;
+  CIR_HIP(dev::launch_verify(d_digests, d_expected, nblk, d_ok, d_nbad, s));
+  return CIR_OK;
+}
+
+int cir_verify_blocks(cir_ctx* ctx, int hash_type, const uint8_t* h_arena, const uint64_t* off,
+                      const uint32_t* len, size_t nblk, const uint8_t* expected, uint8_t* ok_out,
+                      size_t* nbad_out) {
+  if (nblk && !expected) return fail(CIR_EINVAL, "null pointer");
+  std::vector<uint8_t> got(nblk * 32);
+  int rc = cir_hash_blocks_ht(ctx, hash_type, h_arena, off, len, nblk, got.data());
+  if (rc) return rc;
+  size_t nbad = 0;
+  for (size_t b = 0; b < nblk; ++b) {
+    const bool good = memcmp(got.data() + 32 * b, expected + 32 * b, 32) == 0;
+    if (ok_out) ok_out[b] = good ? 1 : 0;
+    nbad += !good;
+  }
+  if (nbad_out) *nbad_out = nbad;
+  return CIR_OK;
+}
+
+int cir_check_file(cir_ctx* ctx, int hash_type, int fd, uint64_t block_size,
+                   const uint8_t* expected, size_t nhash, int* ok_out) {
+  if (!ctx || !ok_out || (nhash && !expected)) return fail(CIR_EINVAL, "null pointer");
+  uint8_t* h = nullptr;
+  size_t n = 0;
+  uint64_t size = 0;
+  int rc = cir_hash_file_ht(ctx, hash_type, fd, block_size, &size, &h, &n);
+  if (rc) return rc;
+  *ok_out = n == nhash && (n == 0 || memcmp(h, expected, 32 * n) == 0);
+  free(h);
+  return CIR_OK;
 }
 
 int cir_debug_hash_uniform_dev(int loader, const void* d_data, uint64_t block_size, uint64_t nblk,

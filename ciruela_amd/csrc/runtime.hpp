@@ -71,9 +71,10 @@ struct Device {
 // block k = h_data[h_off[k] .. h_off[k] + h_len[k]).
 // Staging engine: the caller packs a slot, submit() uploads and hashes it
 // asynchronously, wait() returns the digests in h_out.
-int slot_submit(Device& d, Slot& s, uint64_t bytes, uint64_t nblk);
+int slot_submit(Device& d, Slot& s, uint64_t bytes, uint64_t nblk, int ht = CIR_HASH_BLAKE2B_256);
 int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, const uint32_t* len,
-                      uint64_t n, uint8_t* out, hipStream_t s);
+                      uint64_t n, uint8_t* out, hipStream_t s, int ht = CIR_HASH_BLAKE2B_256);
+bool valid_hash_type(int ht);
 int slot_wait(Device& d, Slot& s);
 
 }  // namespace cir

@@ -179,7 +179,7 @@ static int run_reads(const std::vector<ReadJob>& jobs, const std::vector<ScanFil
 using Progress = std::function<int(uint64_t done_blk)>;
 
 static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, unsigned threads,
-                      std::vector<uint8_t>& digests, const Progress& progress) {
+                      int ht, std::vector<uint8_t>& digests, const Progress& progress) {
   uint64_t nblk_total = 0;
   for (ScanFile& f : files) {
     f.first_blk = nblk_total;
@@ -246,7 +246,7 @@ static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, u
       rc = run_reads(jobs, files, threads);
       if (rc) return rc;
       const double t_read1 = trace_on() ? now_ms() : 0;
-      rc = slot_submit(d, s, std::max<uint64_t>(pos, 16), n);
+      rc = slot_submit(d, s, std::max<uint64_t>(pos, 16), n, ht);
       if (rc) return rc;
       if (trace_on())
         fprintf(stderr, "cir_scan batch: %.1f MiB, %zu jobs, wait %.2f ms, read %.2f ms (%.1f GB/s)\n",
@@ -391,9 +391,12 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
   if (hash_type == CIR_HASH_BLAKE2B_256)
     hdr.hash = dirsig::HashType::kBlake2b256;
   else if (hash_type == CIR_HASH_SHA512_256)
-    return fail(CIR_EUNSUPPORTED, "sha512/256 block hashing is not implemented on the GPU");
+    hdr.hash = dirsig::HashType::kSha512_256;
   else
     return fail(CIR_EINVAL, "unknown hash type");
+  // The incremental footer chain is BLAKE2b (quad mode); a sha512/256 footer
+  // is hashed once at the end (one lane).
+  const bool incremental = hash_type == CIR_HASH_BLAKE2B_256;
   if (threads == 0) threads = std::max(1u, std::thread::hardware_concurrency());
 
   std::vector<PlanItem> plan;
@@ -410,7 +413,7 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
   std::lock_guard<std::mutex> chain_lock(dv.chain_mu);
   CIR_HIP(hipSetDevice(dv.id));
   FooterChain chain(dv);
-  int rc = chain.start();
+  int rc = incremental ? chain.start() : CIR_OK;
   if (rc) return rc;
   std::vector<uint8_t> digests;
   size_t plan_pos = 0;
@@ -430,9 +433,9 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
         em.add_file(it.name, it.exe, f.size, digests.data() + 32 * f.first_blk, nb);
       }
     }
-    return chain.advance(em.body(), (size_t)1 << 20);
+    return incremental ? chain.advance(em.body(), (size_t)1 << 20) : (int)CIR_OK;
   };
-  rc = hash_files(ctx, files, block_size, threads, digests, emit_ready);
+  rc = hash_files(ctx, files, block_size, threads, hash_type, digests, emit_ready);
   if (rc) return rc;
   rc = emit_ready(~0ull);
   if (rc) return rc;
@@ -440,7 +443,13 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
   const std::string& body = em.body();
   if (body.size() - chain.fed > 0xffffffffull) return fail(CIR_EINVAL, "index tail above 4 GiB");
   uint8_t footer[32];
-  rc = chain.finish(body, footer);
+  if (incremental) {
+    rc = chain.finish(body, footer);
+  } else {
+    const uint64_t off = 0;
+    const uint32_t blen = (uint32_t)body.size();
+    rc = cir_hash_blocks_ht(ctx, hash_type, (const uint8_t*)body.data(), &off, &blen, 1, footer);
+  }
   if (rc) return rc;
   const std::string out = em.finish(footer, 32);
   *index_out = (uint8_t*)malloc(out.size());
@@ -457,8 +466,6 @@ int cir_index_rewrite(cir_ctx* ctx, const uint8_t* in, size_t len, uint8_t** out
   dirsig::Index idx;
   std::string err;
   if (!dirsig::parse(in, len, &idx, &err)) return fail(CIR_EPARSE, "ParseError: " + err);
-  if (idx.header.hash != dirsig::HashType::kBlake2b256)
-    return fail(CIR_EUNSUPPORTED, "footer hash sha512/256 is not implemented on the GPU");
   Tree root;
   Tree* cur = &root;
   std::vector<std::string> parts;
@@ -494,8 +501,10 @@ int cir_index_rewrite(cir_ctx* ctx, const uint8_t* in, size_t len, uint8_t** out
   const uint64_t off = 0;
   const uint32_t blen = (uint32_t)body.size();
   static const uint8_t empty = 0;
-  int rc = cir_hash_blocks(ctx, body.empty() ? &empty : (const uint8_t*)body.data(), &off, &blen,
-                           1, footer);
+  const int ht = idx.header.hash == dirsig::HashType::kSha512_256 ? CIR_HASH_SHA512_256
+                                                                   : CIR_HASH_BLAKE2B_256;
+  int rc = cir_hash_blocks_ht(ctx, ht, body.empty() ? &empty : (const uint8_t*)body.data(), &off,
+                              &blen, 1, footer);
   if (rc) return rc;
   const std::string res = em.finish(footer, 32);
   *out = (uint8_t*)malloc(res.size());

@@ -49,7 +49,7 @@ enum cir_status {
 /* dir-signature HashType (external crate 0.2.9; header tokens in the index) */
 enum cir_hash_type {
   CIR_HASH_BLAKE2B_256 = 1, /* HashType::blake2b_256()  "blake2b/256" */
-  CIR_HASH_SHA512_256 = 2   /* HashType::sha512_256()   "sha512/256" (parse only) */
+  CIR_HASH_SHA512_256 = 2   /* HashType::sha512_256()   "sha512/256" */
 };
 
 typedef struct cir_ctx cir_ctx;
@@ -104,6 +104,48 @@ int cir_hash_file(cir_ctx* ctx, int fd, uint64_t block_size, uint64_t* size_out,
 int cir_hash_memory(cir_ctx* ctx, const uint8_t* data, uint64_t size, uint64_t block_size,
                     uint8_t** hashes_out, size_t* nhash_out);
 
+/* ---- other hash types (dir-signature HashType) ------------------------ */
+
+/* The entry points above with an explicit HashType (enum cir_hash_type):
+ * Hashes::hash_file(hash_type, ...) is generic over the index's hash type
+ * (src/cluster/download.rs:257 passes self.hash_type). */
+int cir_sha512_256(const uint8_t* p, size_t n, uint8_t out[CIR_DIGEST_BYTES]);
+int cir_hash_blocks_dev_ht(cir_ctx* ctx, int hash_type, const void* d_arena,
+                           const uint64_t* d_off, const uint32_t* d_len, size_t nblk,
+                           uint8_t* d_out, void* stream);
+int cir_hash_blocks_ht(cir_ctx* ctx, int hash_type, const uint8_t* h_arena, const uint64_t* off,
+                       const uint32_t* len, size_t nblk, uint8_t* h_out);
+int cir_hash_file_ht(cir_ctx* ctx, int hash_type, int fd, uint64_t block_size,
+                     uint64_t* size_out, uint8_t** hashes_out, size_t* nhash_out);
+int cir_hash_memory_ht(cir_ctx* ctx, int hash_type, const uint8_t* data, uint64_t size,
+                       uint64_t block_size, uint8_t** hashes_out, size_t* nhash_out);
+
+/* ---- verification (the daemon side of the same hash) ------------------ */
+
+/* FetchBlock::poll's `BlockHash::hash_bytes(&data.data) == blk.hash`
+ * (src/daemon/tracking/fetch_blocks.rs:77) over a device-resident batch of
+ * received blocks: the blocks are hashed (as cir_hash_blocks_dev_ht) into
+ * d_digests (32 x nblk bytes of scratch) and compared with d_expected on the
+ * same stream.  d_ok[b] = 1 when block b matches, 0 when it does not (the
+ * reference then retries the block elsewhere, :91-103); *d_nbad (device
+ * u32) = number of mismatches.  d_ok / d_nbad may be NULL.  d_expected and
+ * d_digests must be 16-byte aligned. */
+int cir_verify_blocks_dev(cir_ctx* ctx, int hash_type, const void* d_arena, const uint64_t* d_off,
+                          const uint32_t* d_len, size_t nblk, const uint8_t* d_expected,
+                          uint8_t* d_digests, uint8_t* d_ok, uint32_t* d_nbad, void* stream);
+
+/* Host-memory batch of the same check; ok_out (nblk bytes) may be NULL. */
+int cir_verify_blocks(cir_ctx* ctx, int hash_type, const uint8_t* h_arena, const uint64_t* off,
+                      const uint32_t* len, size_t nblk, const uint8_t* expected, uint8_t* ok_out,
+                      size_t* nbad_out);
+
+/* Hashes::check_file(&mut file) at image commit (src/daemon/disk/commit.rs:
+ * 104; false -> Error::Checksum, :110): re-hash fd from its current offset to
+ * EOF in block_size blocks; *ok_out = 1 iff the file has exactly nhash
+ * blocks and every digest equals expected[32 i .. 32 i + 32]. */
+int cir_check_file(cir_ctx* ctx, int hash_type, int fd, uint64_t block_size,
+                   const uint8_t* expected, size_t nhash, int* ok_out);
+
 /* ---- index (DIRSIGNATURE.v1) ----------------------------------------- */
 
 /* dir_signature::v1::scan(&ScannerConfig, &mut Vec<u8>)
@@ -124,7 +166,7 @@ int cir_index_get_hash(const uint8_t* index, size_t len, uint8_t* id_out, size_t
  * 171-188, 266-319): parse, rebuild the directory tree and re-emit it in the
  * reference's order (files and links by name, then subdirectories; empty
  * directories dropped) with the footer recomputed on the GPU.  blake2b/256
- * indexes only (CIR_EUNSUPPORTED for sha512/256 until its kernel exists). */
+ * and sha512/256 indexes (the footer is hashed with the index's hash type). */
 int cir_index_rewrite(cir_ctx* ctx, const uint8_t* in, size_t len, uint8_t** out, size_t* out_len);
 
 /* ---- consumers of the index (host bookkeeping) ------------------------ */

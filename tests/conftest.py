@@ -42,6 +42,7 @@ def oracle():
     lib.oracle_hash_blocks.argtypes = [vp, vp, vp, ctypes.c_size_t, vp, ctypes.c_int]
     lib.oracle_hash_chunks.argtypes = [vp, u64, u64, vp, ctypes.c_int]
     lib.oracle_splitmix64_fill.argtypes = [vp, u64, u64, u64, u64, u64]
+    lib.oracle_sha512_256.argtypes = [vp, vp, ctypes.c_size_t]
     return lib
 
 
@@ -49,6 +50,13 @@ def oracle_digest(lib, data):
     out = ctypes.create_string_buffer(32)
     buf = ctypes.create_string_buffer(bytes(data), max(len(data), 1))
     lib.oracle_blake2b256(out, buf, len(data))
+    return out.raw
+
+
+def oracle_sha(lib, data):
+    out = ctypes.create_string_buffer(32)
+    buf = ctypes.create_string_buffer(bytes(data), max(len(data), 1))
+    lib.oracle_sha512_256(out, buf, len(data))
     return out.raw
 
 

@@ -11,7 +11,7 @@ import random
 import numpy as np
 import pytest
 
-from conftest import oracle_digest
+from conftest import oracle_digest, oracle_sha
 from make_golden import gen_bytes
 
 import dirsig_oracle
@@ -310,3 +310,117 @@ def test_cli_sync(gpu, tmp_path):
     assert (tmp_path / (image_id + ".ds1")).read_bytes() == want
     assert kind == "append" and dest == "/dest"
     assert want.endswith(image_id.encode() + b"\n")
+
+
+def test_sha512_256_single_and_batches(gpu, ctx, oracle):
+    """dir-signature's second hash type on the GPU vs the oracle."""
+    import torch
+    sha = gpu.HashType.sha512_256()
+    for n in [0, 1, 7, 111, 112, 113, 127, 128, 129, 239, 240, 255, 256, 1000, 32768]:
+        d = os.urandom(n)
+        assert gpu.sha512_256(d) == oracle_sha(oracle, d), n
+    rng = random.Random(9)
+    lens = [rng.choice([0, 1, 111, 112, 128, 4096, 32768, rng.randrange(0, 70000)])
+            for _ in range(1500)]
+    arena = os.urandom(sum(lens) + 64)
+    offs, pos = [], 0
+    for ln in lens:
+        offs.append(pos)
+        pos += ln
+    got = ctx.hash_blocks(arena, offs, lens, hash_type=sha)
+    for i in range(0, len(lens), 7):
+        assert got[32 * i:32 * i + 32] == oracle_sha(oracle, arena[offs[i]:offs[i] + lens[i]]), i
+    # device-resident descriptors
+    t = torch.tensor(bytearray(arena), dtype=torch.uint8, device="cuda:0")
+    d_off = torch.tensor(offs, dtype=torch.int64, device="cuda:0")
+    d_len = torch.tensor(lens, dtype=torch.int32, device="cuda:0")
+    out = torch.zeros(32 * len(lens), dtype=torch.uint8, device="cuda:0")
+    ctx.hash_blocks_dev(t.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), len(lens),
+                        out.data_ptr(), 0, hash_type=sha)
+    torch.cuda.synchronize()
+    assert out.cpu().numpy().tobytes() == got
+    data = os.urandom(5 * 32768 + 17)
+    assert ctx.hash_memory(data, 32768, hash_type=sha) == b"".join(
+        oracle_sha(oracle, data[i:i + 32768]) for i in range(0, len(data), 32768))
+
+
+def test_reference_roundtrip_fixture_on_gpu(gpu, small_ctx, dirsig_example):
+    """The reference's own test, src/cluster/download.rs:368-382 (`roundtrip`):
+    RawIndex::into_mut + to_raw_data reproduces EXAMPLE byte for byte -- here
+    parsed, re-emitted and re-footed (SHA-512/256 on the GPU)."""
+    idx = dirsig_example["index"].encode()
+    assert small_ctx.index_rewrite(idx) == idx
+
+
+def test_scan_sha512(gpu, small_ctx, tmp_path):
+    make_tree(tmp_path)
+    cfg = gpu.ScannerConfig.new().hash(gpu.HashType.sha512_256()).add_dir(str(tmp_path), "/")
+    assert gpu.v1.scan(cfg, context=small_ctx) == \
+        dirsig_oracle.scan(str(tmp_path), 32768, hash_name="sha512/256")
+
+
+def _corrupt(b, i):
+    return b[:i] + bytes([b[i] ^ 0x01]) + b[i + 1:]
+
+
+@pytest.mark.parametrize("ht", ["blake2b", "sha512"])
+def test_verify_blocks_host_and_device(gpu, ctx, oracle, ht):
+    """Row f2: fetch_blocks.rs:77 `hash_bytes(&data) == blk.hash`, batched."""
+    import torch
+    hasht = gpu.HashType.blake2b_256() if ht == "blake2b" else gpu.HashType.sha512_256()
+    dig = (lambda d: oracle_digest(oracle, d)) if ht == "blake2b" else \
+        (lambda d: oracle_sha(oracle, d))
+    rng = random.Random(21)
+    lens = [rng.choice([0, 1, 127, 128, 4096, 32768, rng.randrange(0, 40000)])
+            for _ in range(700)]
+    arena = os.urandom(sum(lens) + 16)
+    offs, pos = [], 0
+    for ln in lens:
+        offs.append(pos)
+        pos += ln
+    expected = b"".join(dig(arena[o:o + ln]) for o, ln in zip(offs, lens))
+    bad = set(rng.sample(range(len(lens)), 37))
+    exp_bad = expected
+    for b in bad:
+        exp_bad = _corrupt(exp_bad, 32 * b + rng.randrange(32))
+    assert ctx.verify_blocks(arena, offs, lens, expected, hash_type=hasht) == [True] * len(lens)
+    ok = ctx.verify_blocks(arena, offs, lens, exp_bad, hash_type=hasht)
+    assert [i for i, g in enumerate(ok) if not g] == sorted(bad)
+    # device-resident: received blocks in HBM, expected digests in HBM
+    t = torch.tensor(bytearray(arena), dtype=torch.uint8, device="cuda:0")
+    d_off = torch.tensor(offs, dtype=torch.int64, device="cuda:0")
+    d_len = torch.tensor(lens, dtype=torch.int32, device="cuda:0")
+    d_exp = torch.tensor(bytearray(exp_bad), dtype=torch.uint8, device="cuda:0")
+    d_dig = torch.zeros(32 * len(lens), dtype=torch.uint8, device="cuda:0")
+    d_ok = torch.full((len(lens),), 7, dtype=torch.uint8, device="cuda:0")
+    d_nbad = torch.full((1,), 12345, dtype=torch.int32, device="cuda:0")
+    ctx.verify_blocks_dev(t.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), len(lens),
+                          d_exp.data_ptr(), d_dig.data_ptr(), d_ok.data_ptr(),
+                          d_nbad.data_ptr(), hash_type=hasht)
+    torch.cuda.synchronize()
+    assert d_dig.cpu().numpy().tobytes() == expected
+    assert [i for i, g in enumerate(d_ok.cpu().tolist()) if g != 1] == sorted(bad)
+    assert set(d_ok.cpu().tolist()) <= {0, 1}
+    assert int(d_nbad.item()) == len(bad)
+
+
+def test_check_file_commit(gpu, small_ctx, tmp_path):
+    """Row f2: Hashes::check_file at commit (src/daemon/disk/commit.rs:104)."""
+    data = os.urandom(3 * 32768 + 999)
+    p = tmp_path / "f"
+    p.write_bytes(data)
+    for ht in (gpu.HashType.blake2b_256(), gpu.HashType.sha512_256()):
+        with open(p, "rb") as f:
+            size, hashes = gpu.Hashes.hash_file(ht, 32768, f, context=small_ctx)
+        assert size == len(data) and len(hashes) == 4
+        with open(p, "rb") as f:
+            assert hashes.check_file(f, context=small_ctx)
+        for bad in (_corrupt(data, 40000), data[:-1], data + b"x", data[:3 * 32768]):
+            q = tmp_path / "g"
+            q.write_bytes(bad)
+            with open(q, "rb") as f:
+                assert not hashes.check_file(f, context=small_ctx)
+    empty = tmp_path / "e"
+    empty.write_bytes(b"")
+    with open(empty, "rb") as f:
+        assert gpu.Hashes(b"", 32768).check_file(f, context=small_ctx)

@@ -13,7 +13,7 @@ import struct
 
 import numpy as np
 
-from conftest import oracle_digest
+from conftest import oracle_digest, oracle_sha
 from make_golden import RFC7693_ABC_512, gen_bytes, splitmix64_words
 
 
@@ -100,3 +100,16 @@ def test_splitmix_host_twin(oracle):
         assert list(buf[8 * b:8 * b + 8]) == splitmix64_words(0x5EED0004 ^ (5 + b), 8)
     raw = struct.pack("<4Q", *splitmix64_words(7, 4))
     assert gen_bytes({"gen": "splitmix64", "n": 32, "seed": 7}) == raw
+
+
+def test_sha512_256_oracle(oracle, dirsig_example):
+    """Second hash type (FIPS 180-4): hashlib and the reference fixture."""
+    for n in list(range(0, 260)) + [1000, 32768, 100000]:
+        d = os.urandom(n)
+        assert oracle_sha(oracle, d) == hashlib.new("sha512_256", d).digest(), n
+    # reference fixture, src/cluster/download.rs:363: ".hidden f 7 6d7f5f98..."
+    assert oracle_sha(oracle, b"Hidden\n").hex() == \
+        "6d7f5f9804ee4dbc1ff7e12c7665387e0119e8ea629996c52d38b75c12ad0acf"
+    idx = dirsig_example["index"].encode()
+    body = idx[idx.index(b"\n") + 1:-65]
+    assert oracle_sha(oracle, body).hex().encode() == idx[-65:-1]

@@ -26,6 +26,8 @@ for s in "$@"; do
   case "$s" in
     diag)
       step diag 400 python -X faulthandler tools/diag.py ;;
+    shadiag)
+      step shadiag 300 python tools/sha_diag.py ;;
     cli)
       head -c 100000 /dev/urandom > /tmp/cli_probe.bin
       step cli 120 ./bin/ciruela-index hash /tmp/cli_probe.bin ;;
