@@ -108,7 +108,10 @@ static int walk(const std::string& real, const std::string& vpath, std::vector<P
 constexpr uint64_t kReadPiece = 4ull << 20;
 
 static bool trace_on() {
-  static const bool on = std::getenv("CIR_TRACE") != nullptr;
+  static const bool on = [] {
+    const char* v = std::getenv("CIR_TRACE");
+    return v && *v && strcmp(v, "0") != 0;
+  }();
   return on;
 }
 
@@ -399,6 +402,7 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
   const bool incremental = hash_type == CIR_HASH_BLAKE2B_256;
   if (threads == 0) threads = std::max(1u, std::thread::hardware_concurrency());
 
+  const double t0 = trace_on() ? now_ms() : 0;
   std::vector<PlanItem> plan;
   std::vector<ScanFile> files;
   for (size_t i = 0; i < ndirs; ++i) {
@@ -435,10 +439,13 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
     }
     return incremental ? chain.advance(em.body(), (size_t)1 << 20) : (int)CIR_OK;
   };
+  const double t1 = trace_on() ? now_ms() : 0;
   rc = hash_files(ctx, files, block_size, threads, hash_type, digests, emit_ready);
   if (rc) return rc;
+  const double t2 = trace_on() ? now_ms() : 0;
   rc = emit_ready(~0ull);
   if (rc) return rc;
+  const double t3 = trace_on() ? now_ms() : 0;
   // Footer = H(every byte after the header line), finished on the GPU.
   const std::string& body = em.body();
   if (body.size() - chain.fed > 0xffffffffull) return fail(CIR_EINVAL, "index tail above 4 GiB");
@@ -451,11 +458,18 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
     rc = cir_hash_blocks_ht(ctx, hash_type, (const uint8_t*)body.data(), &off, &blen, 1, footer);
   }
   if (rc) return rc;
+  const double t4 = trace_on() ? now_ms() : 0;
   const std::string out = em.finish(footer, 32);
   *index_out = (uint8_t*)malloc(out.size());
   if (!*index_out) return fail(CIR_ENOMEM, "malloc");
   memcpy(*index_out, out.data(), out.size());
   *len_out = out.size();
+  if (trace_on())
+    fprintf(stderr,
+            "cir_scan phases: walk %.1f ms, hash loop %.1f ms, last emit %.1f ms, footer %.1f ms, "
+            "output %.1f ms; %zu files, index %.1f MiB\n",
+            t1 - t0, t2 - t1, t3 - t2, t4 - t3, now_ms() - t4, files.size(),
+            out.size() / 1048576.0);
   return CIR_OK;
 }
 

@@ -26,6 +26,18 @@ for s in "$@"; do
   case "$s" in
     diag)
       step diag 400 python -X faulthandler tools/diag.py ;;
+    ablib)
+      step ablib 600 python tools/ab_lib.py abtest/*.so > gpurun_out/ablib.log 2>&1
+      cat gpurun_out/ablib.log ;;
+    h2d)
+      step h2d 300 python tools/h2d_probe.py > gpurun_out/h2d.log 2>&1
+      HSA_ENABLE_SDMA=0 step h2d_blit 300 python tools/h2d_probe.py > gpurun_out/h2d_blit.log 2>&1
+      cat gpurun_out/h2d.log gpurun_out/h2d_blit.log ;;
+    cfg5blit)
+      HSA_ENABLE_SDMA=0 step cfg5blit 1000 python bench.py --workload config5 --steps 3 \
+        --tree-gib "${TREE_GIB:-50}" > gpurun_out/cfg5blit.json 2> gpurun_out/cfg5blit.err
+      rm -rf /dev/shm/ciruela_bench_tree
+      cat gpurun_out/cfg5blit.json ;;
     shadiag)
       step shadiag 300 python tools/sha_diag.py ;;
     cli)
@@ -67,7 +79,7 @@ for s in "$@"; do
     cfg5)
       df -h /dev/shm /tmp | tee gpurun_out/df.txt
       free -g | tee -a gpurun_out/df.txt
-      step cfg5 1000 python bench.py --workload config5 --steps 3 --tree-gib "${TREE_GIB:-50}" \
+      CIR_TRACE=${CIR_TRACE:-} step cfg5 1000 python bench.py --workload config5 --steps 3 --tree-gib "${TREE_GIB:-50}" \
         > gpurun_out/cfg5.json 2> gpurun_out/cfg5.err
       rm -rf /dev/shm/ciruela_bench_tree
       cat gpurun_out/cfg5.json ;;
