@@ -155,6 +155,25 @@ def config3_layout(total=10 << 30, seed=0x5EED0003):
     return offs, lens.astype(np.int32), int(offs[-1] + padded[-1])
 
 
+def valu_ceiling(ca, nblk, bs, stream, reps=4):
+    """Median time of nblk x ceil(bs/128) register-only compressions (the
+    kernel's VALU work with no loads): the measured VALU ceiling."""
+    import torch
+    if nblk % 256 or bs % 128:
+        return None
+    buf = torch.empty(32 * nblk, dtype=torch.uint8, device=torch.cuda.current_device())
+    ts = []
+    for i in range(reps + 1):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        ca._n.check(ca._n.lib.cir_debug_compress_only_dev(nblk, bs // 128, buf.data_ptr(), stream))
+        b.record()
+        b.synchronize()
+        if i:
+            ts.append(a.elapsed_time(b))
+    return round(sorted(ts)[len(ts) // 2], 4)
+
+
 def run_config3(args, ca, ctx, dev, stream):
     import torch
     offs, lens, nbytes = config3_layout()
@@ -354,6 +373,7 @@ def main():
                 parity = "FAIL: golden config-2 blocks differ"
     if parity != "ok":
         log("PARITY " + parity)
+    valu_ms = valu_ceiling(ca, nblk, bs, stream)
 
     if rank == 0:
         avg_kern_s = sum(kern_ms) / len(kern_ms) / 1e3
@@ -389,8 +409,12 @@ def main():
                 "traffic": traffic,
                 "kernel_ms_avg": round(avg_kern_s * 1e3, 4),
                 "kernel_ms_min": round(min(kern_ms), 4),
+                "valu_ceiling_ms": valu_ms,
+                "valu_frac": round(valu_ms / (avg_kern_s * 1e3), 4) if valu_ms else None,
                 "note": "binding roof is integer VALU (~2.0k VALU ops per 128-B "
-                        "compression), see DESIGN.md",
+                        "compression): valu_ceiling_ms = the same number of "
+                        "compressions in registers with no memory traffic, timed "
+                        "live; valu_frac = valu_ceiling_ms / kernel_ms_avg; see DESIGN.md",
             },
             "parity": parity,
         }

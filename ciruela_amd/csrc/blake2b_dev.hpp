@@ -282,12 +282,14 @@ constexpr int kQuadFromNext = 0x39;   // lane i <- lane i+1  (quad_perm [1,2,3,0
 constexpr int kQuadFromNext2 = 0x4E;  // lane i <- lane i+2  (quad_perm [2,3,0,1])
 constexpr int kQuadFromPrev = 0x93;   // lane i <- lane i+3  (quad_perm [3,0,1,2])
 
+// (a + m) + b: the message add does not wait for b, so only one 64-bit add
+// per half-G sits on the chain's critical path (quad mode is latency-bound).
 #define CIR_GQ(x, y)                  \
-  a = a + b + (x);                    \
+  a = (a + (x)) + b;                  \
   d = xor_rotr<32, 0>(d, a);          \
   c = c + d;                          \
   b = xor_rotr<24, 0>(b, c);          \
-  a = a + b + (y);                    \
+  a = (a + (y)) + b;                  \
   d = xor_rotr<16, 0>(d, a);          \
   c = c + d;                          \
   b = xor_rotr<63, 0>(b, c);
@@ -295,21 +297,39 @@ constexpr int kQuadFromPrev = 0x93;   // lane i <- lane i+3  (quad_perm [3,0,1,2
 // One compression of the chain owned by this quad.  line = the quad's 128-B
 // message line in LDS; addr[r*4 + k] = byte offset of the k-th word lane i
 // needs in round r.  cv/dv = IV[i]/IV[4+i]; dmask = this lane's t / final-flag
-// contribution to v[12+i].
-__device__ __forceinline__ void compress_quad(uint64_t& h0, uint64_t& h1, const uint8_t* line,
-                                              const uint32_t (&addr)[48], uint64_t cv,
-                                              uint64_t dv) {
+// contribution to v[12+i].  kPrefetchAll: issue all 48 LDS reads before the
+// first round (+96 VGPRs) so no round waits on LDS latency -- for the
+// single-chain footer kernel, whose one wave has registers to spare.
+template <bool kPrefetchAll>
+__device__ __forceinline__ void compress_quad_t(uint64_t& h0, uint64_t& h1, const uint8_t* line,
+                                                const uint32_t (&addr)[48], uint64_t cv,
+                                                uint64_t dv) {
   uint64_t a = h0, b = h1, c = cv, d = dv;
+  uint64_t msg[kPrefetchAll ? 48 : 1];
+  if constexpr (kPrefetchAll) {
+#pragma unroll
+    for (int k = 0; k < 48; ++k) msg[k] = *reinterpret_cast<const uint64_t*>(line + addr[k]);
+    // consume every word here: the scheduler cannot sink the reads back into
+    // the rounds, so the compression waits on LDS once instead of per round
+#pragma unroll
+    for (int k = 0; k < 48; ++k) asm volatile("" : "+v"(msg[k]));
+  }
+  auto word = [&](int k) -> uint64_t {
+    if constexpr (kPrefetchAll)
+      return msg[k];
+    else
+      return *reinterpret_cast<const uint64_t*>(line + addr[k]);
+  };
 #pragma unroll
   for (int r = 0; r < 12; ++r) {
-    const uint64_t x0 = *reinterpret_cast<const uint64_t*>(line + addr[4 * r + 0]);
-    const uint64_t y0 = *reinterpret_cast<const uint64_t*>(line + addr[4 * r + 1]);
+    const uint64_t x0 = word(4 * r + 0);
+    const uint64_t y0 = word(4 * r + 1);
     CIR_GQ(x0, y0)
     b = qperm<kQuadFromNext>(b);
     c = qperm<kQuadFromNext2>(c);
     d = qperm<kQuadFromPrev>(d);
-    const uint64_t x1 = *reinterpret_cast<const uint64_t*>(line + addr[4 * r + 2]);
-    const uint64_t y1 = *reinterpret_cast<const uint64_t*>(line + addr[4 * r + 3]);
+    const uint64_t x1 = word(4 * r + 2);
+    const uint64_t y1 = word(4 * r + 3);
     CIR_GQ(x1, y1)
     b = qperm<kQuadFromPrev>(b);
     c = qperm<kQuadFromNext2>(c);
@@ -317,6 +337,12 @@ __device__ __forceinline__ void compress_quad(uint64_t& h0, uint64_t& h1, const 
   }
   h0 = xor3(h0, a, c);
   h1 = xor3(h1, b, d);
+}
+
+__device__ __forceinline__ void compress_quad(uint64_t& h0, uint64_t& h1, const uint8_t* line,
+                                              const uint32_t (&addr)[48], uint64_t cv,
+                                              uint64_t dv) {
+  compress_quad_t<false>(h0, h1, line, addr, cv, dv);
 }
 
 // Bytes [32k, 32k + 32) of a line at p, of which the first n (0..32) are

@@ -157,6 +157,7 @@ __device__ __forceinline__ void quad_init(uint32_t i, uint64_t& h0, uint64_t& h1
 // Advance a quad's chain over L bytes at p, t0 bytes already compressed.
 // final: the last line (partial, or the empty block of an empty input)
 // carries the final flag; otherwise L must be a multiple of 128.
+template <bool kPrefetchAll = false>
 __device__ __forceinline__ void quad_run(uint64_t& h0, uint64_t& h1, uint64_t t0,
                                          const uint8_t* p, uint32_t L, bool active, bool final,
                                          uint8_t* lds, const uint32_t (&addr)[48], uint32_t line,
@@ -182,7 +183,7 @@ __device__ __forceinline__ void quad_run(uint64_t& h0, uint64_t& h1, uint64_t t0
     const bool last = final && it + 1 == total;
     const uint64_t t = t0 + (last ? (uint64_t)L : (uint64_t)(it + 1) * 128u);
     const uint64_t dv = dv0 ^ (i == 0 ? t : 0ull) ^ ((i == 2 && last) ? ~0ull : 0ull);
-    compress_quad(h0, h1, lds, addr, cv, dv);
+    compress_quad_t<kPrefetchAll>(h0, h1, lds, addr, cv, dv);
   }
 }
 
@@ -239,7 +240,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_mixed(const uint8_t* __restrict
 // Resumable single chain (the index footer, fed incrementally): one quad.
 // st[0..7] = chain value, st[8] = bytes compressed so far.  After the final
 // call st[0..3] is the digest.
-__global__ __launch_bounds__(64) void k_chain_step(uint64_t* __restrict__ st,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_chain_step(uint64_t* __restrict__ st,
                                                    const uint8_t* __restrict__ data, uint32_t n,
                                                    int final) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[128];
@@ -250,7 +251,7 @@ __global__ __launch_bounds__(64) void k_chain_step(uint64_t* __restrict__ st,
   const uint64_t t0 = st[8];
   uint64_t h0 = st[i], h1 = st[4 + i];
   if (t0 == 0 && st[9] == 0) quad_init(i, h0, h1);  // st[9] = 0: fresh state
-  quad_run(h0, h1, t0, data, n, true, final != 0, lds, addr, 0u, i);
+  quad_run<true>(h0, h1, t0, data, n, true, final != 0, lds, addr, 0u, i);
   st[i] = h0;
   st[4 + i] = h1;
   if (i == 0) {
@@ -285,6 +286,30 @@ hipError_t launch_sha_desc(const uint8_t* arena, const uint64_t* off, const uint
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_sha_desc, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, arena, off,
                      len, perm, n, out);
+  return hipGetLastError();
+}
+
+// Register-only compressions (no memory traffic): `lines` compressions per
+// lane on a message kept in registers -- the measured VALU ceiling the bench
+// reports next to the HBM roofline (diagnostics, not part of the reference).
+__global__ __launch_bounds__(kThreads, 5) void k_compress_only(uint8_t* __restrict__ out,
+                                                              uint32_t lines) {
+  const uint64_t b = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+  uint64_t h[8], m[16];
+  init_state(h);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) m[k] = b * 0x9e3779b97f4a7c15ULL + k;
+  for (uint32_t i = 0; i < lines; ++i) {
+    m[0] ^= i;  // keep the message live and varying (static index: no scratch)
+    compress(h, m, (uint64_t)(i + 1) * 128u, i + 1 == lines);
+  }
+  store_digest(out + b * 32u, h);
+}
+
+hipError_t launch_compress_only(uint64_t nlanes, uint32_t lines, uint8_t* out, hipStream_t s) {
+  if (nlanes == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_compress_only, dim3(grid_for(nlanes, kThreads)), dim3(kThreads), 0, s, out,
+                     lines);
   return hipGetLastError();
 }
 

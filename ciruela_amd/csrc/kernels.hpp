@@ -63,6 +63,9 @@ hipError_t launch_chain_step(uint64_t* st, const uint8_t* data, uint32_t n, bool
 hipError_t launch_verify(const uint8_t* got, const uint8_t* want, uint64_t n, uint8_t* ok,
                          uint32_t* nbad, hipStream_t s);
 
+// nlanes x `lines` register-only compressions (diagnostic VALU ceiling).
+hipError_t launch_compress_only(uint64_t nlanes, uint32_t lines, uint8_t* out, hipStream_t s);
+
 hipError_t launch_fill_splitmix64(uint64_t* p, uint64_t nwords, uint64_t seed,
                                   uint64_t block_words, uint64_t first_block, hipStream_t s);
 

@@ -41,6 +41,8 @@ Device::~Device() {
     (void)hipFree(s.d_out);
     if (s.copied) (void)hipEventDestroy(s.copied);
     if (s.done) (void)hipEventDestroy(s.done);
+    for (hipEvent_t e : {s.t_copy0, s.t_copy1, s.t_hash0})
+      if (e) (void)hipEventDestroy(e);
   }
   if (chain) (void)hipStreamSynchronize(chain);
   for (int k = 0; k < 2; ++k) {
@@ -57,10 +59,23 @@ Device::~Device() {
   if (copy) (void)hipStreamDestroy(copy);
 }
 
+bool trace_enabled() {
+  static const bool on = [] {
+    const char* v = std::getenv("CIR_TRACE");
+    return v && *v && strcmp(v, "0") != 0;
+  }();
+  return on;
+}
+
 int Device::ensure_slot(Slot& s, uint64_t bytes, uint64_t nblk) {
   if (!s.copied) {
     CIR_HIP(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
-    CIR_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+    CIR_HIP(hipEventCreateWithFlags(&s.done, trace_enabled() ? 0 : hipEventDisableTiming));
+    if (trace_enabled()) {
+      CIR_HIP(hipEventCreate(&s.t_copy0));
+      CIR_HIP(hipEventCreate(&s.t_copy1));
+      CIR_HIP(hipEventCreate(&s.t_hash0));
+    }
   }
   if (bytes > s.cap) {
     (void)hipHostFree(s.h_data);
@@ -134,13 +149,16 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
 // bytes of one file split into chunk_bs blocks (nblk = ceil(bytes / bs)).
 static int slot_submit_impl(Device& d, Slot& s, uint64_t bytes, uint64_t nblk,
                             uint64_t chunk_bs, int ht) {
+  if (s.t_copy0) CIR_HIP(hipEventRecord(s.t_copy0, d.copy));
   CIR_HIP(hipMemcpyAsync(s.d_data, s.h_data, bytes, hipMemcpyHostToDevice, d.copy));
   if (chunk_bs == 0) {
     CIR_HIP(hipMemcpyAsync(s.d_off, s.h_off, nblk * 8, hipMemcpyHostToDevice, d.copy));
     CIR_HIP(hipMemcpyAsync(s.d_len, s.h_len, nblk * 4, hipMemcpyHostToDevice, d.copy));
   }
+  if (s.t_copy1) CIR_HIP(hipEventRecord(s.t_copy1, d.copy));
   CIR_HIP(hipEventRecord(s.copied, d.copy));
   CIR_HIP(hipStreamWaitEvent(d.compute, s.copied, 0));
+  if (s.t_hash0) CIR_HIP(hipEventRecord(s.t_hash0, d.compute));
   if (chunk_bs == 0) {
     int rc = hash_desc_ordered(d, s.d_data, s.d_off, s.d_len, nblk, s.d_out, d.compute, ht);
     if (rc) return rc;
@@ -598,6 +616,13 @@ int cir_debug_hash_uniform_dev(int loader, const void* d_data, uint64_t block_si
     return fail(CIR_EINVAL, "uniform kernel needs bs % 128 == 0, nblk % 256 == 0, 16-B alignment");
   CIR_HIP(dev::launch_uniform(loader == 0 ? dev::Loader::kGlds : dev::Loader::kDirect,
                               (const uint8_t*)d_data, block_size, nblk, d_out, (hipStream_t)stream));
+  return CIR_OK;
+}
+
+int cir_debug_compress_only_dev(uint64_t nlanes, uint32_t lines, uint8_t* d_out, void* stream) {
+  if (nlanes % dev::kThreads || lines == 0 || !d_out)
+    return fail(CIR_EINVAL, "compress-only kernel needs nlanes % 256 == 0, lines > 0, an output");
+  CIR_HIP(dev::launch_compress_only(nlanes, lines, d_out, (hipStream_t)stream));
   return CIR_OK;
 }
 

@@ -40,14 +40,22 @@ struct Slot {
   uint64_t cap_blk = 0;
   hipEvent_t copied = nullptr;  // H2D of this slot finished (copy stream)
   hipEvent_t done = nullptr;    // digests of this slot are back in h_out
+  // timing events, recorded only when CIR_TRACE is set (trace_enabled())
+  hipEvent_t t_copy0 = nullptr, t_copy1 = nullptr, t_hash0 = nullptr;
   bool busy = false;
 };
+
+// CIR_TRACE set to a non-empty value other than "0": per-batch timings on stderr.
+bool trace_enabled();
 
 struct Device {
   int id = 0;
   hipStream_t compute = nullptr;
   hipStream_t copy = nullptr;
-  Slot slot[2];
+  // staging slots: the batch entry points cycle through two; the directory
+  // scan through all three (reads of batch k+1 overlap the H2D of k and k-1).
+  static constexpr int kSlots = 3;
+  Slot slot[kSlots];
   std::mutex mu;  // one host-path user at a time per device
   // device scratch of the descriptor ordering (cir_hash_blocks_dev); users on
   // different streams are ordered through `order_free`.

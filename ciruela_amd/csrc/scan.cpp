@@ -107,13 +107,7 @@ static int walk(const std::string& real, const std::string& vpath, std::vector<P
 // readers stay busy on trees of large files.
 constexpr uint64_t kReadPiece = 4ull << 20;
 
-static bool trace_on() {
-  static const bool on = [] {
-    const char* v = std::getenv("CIR_TRACE");
-    return v && *v && strcmp(v, "0") != 0;
-  }();
-  return on;
-}
+static bool trace_on() { return trace_enabled(); }
 
 static double now_ms() {
   return std::chrono::duration<double, std::milli>(
@@ -197,8 +191,14 @@ static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, u
   const uint64_t cap_blk = std::max<uint64_t>(cap / 512, 4096);
   size_t fi = 0;       // current file
   uint64_t fblk = 0;   // next block within it
-  uint64_t pending_first[2] = {0, 0}, pending_n[2] = {0, 0};
+  constexpr int kS = Device::kSlots;
+  uint64_t pending_first[kS] = {}, pending_n[kS] = {};
   int k = 0;
+  auto busy = [&] {
+    for (const Slot& s : d.slot)
+      if (s.busy) return true;
+    return false;
+  };
   auto more = [&] {
     while (fi < files.size() && fblk * bs >= files[fi].size) {
       ++fi;
@@ -206,12 +206,20 @@ static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, u
     }
     return fi < files.size();
   };
-  while (more() || d.slot[0].busy || d.slot[1].busy) {
+  while (more() || busy()) {
     Slot& s = d.slot[k];
     const double t_wait0 = trace_on() ? now_ms() : 0;
     if (s.busy) {
       int rc = slot_wait(d, s);
       if (rc) return rc;
+      if (trace_on() && s.t_copy0) {
+        float copy_ms = 0, hash_ms = 0, gap_ms = 0;
+        (void)hipEventElapsedTime(&copy_ms, s.t_copy0, s.t_copy1);
+        (void)hipEventElapsedTime(&gap_ms, s.t_copy1, s.t_hash0);
+        (void)hipEventElapsedTime(&hash_ms, s.t_hash0, s.done);
+        fprintf(stderr, "cir_scan slot %d: h2d %.2f ms, h2d->hash %.2f ms, hash+d2h %.2f ms\n", k,
+                copy_ms, gap_ms, hash_ms);
+      }
       memcpy(digests.data() + 32 * pending_first[k], s.h_out, 32 * pending_n[k]);
       rc = progress(pending_first[k] + pending_n[k]);
       if (rc) return rc;
@@ -258,7 +266,7 @@ static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, u
       pending_first[k] = first;
       pending_n[k] = n;
     }
-    k ^= 1;
+    k = (k + 1) % kS;
   }
   return CIR_OK;
 }

@@ -212,6 +212,12 @@ int cir_fill_splitmix64_dev(void* d_ptr, uint64_t nbytes, uint64_t seed, uint64_
 int cir_debug_hash_uniform_dev(int loader, const void* d_data, uint64_t block_size, uint64_t nblk,
                                uint8_t* d_out, void* stream);
 
+/* nlanes (% 256 == 0) independent chains of `lines` BLAKE2b compressions on
+ * register-resident messages, digest per lane -> d_out + 32 lane: the same
+ * compression count as hashing nlanes blocks of 128 x lines bytes, with no
+ * memory traffic.  bench.py times it as the measured VALU ceiling. */
+int cir_debug_compress_only_dev(uint64_t nlanes, uint32_t lines, uint8_t* d_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

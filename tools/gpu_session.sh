@@ -38,6 +38,13 @@ for s in "$@"; do
         --tree-gib "${TREE_GIB:-50}" > gpurun_out/cfg5blit.json 2> gpurun_out/cfg5blit.err
       rm -rf /dev/shm/ciruela_bench_tree
       cat gpurun_out/cfg5blit.json ;;
+    batch)
+      step batch 300 python tools/batch_probe.py > gpurun_out/batch.log 2>&1
+      cat gpurun_out/batch.log ;;
+    hostreg)
+      step hostreg 300 python tools/hostreg_probe.py > gpurun_out/hostreg.log 2>&1
+      rm -f /dev/shm/hostreg_probe.bin
+      cat gpurun_out/hostreg.log ;;
     shadiag)
       step shadiag 300 python tools/sha_diag.py ;;
     cli)
