@@ -187,6 +187,7 @@ __device__ __forceinline__ void quad_run(uint64_t& h0, uint64_t& h1, uint64_t t0
   }
 }
 
+template <bool kPrefetchAll>
 __device__ __forceinline__ void quad_chains(const uint8_t* __restrict__ arena,
                                             const uint64_t* __restrict__ off,
                                             const uint32_t* __restrict__ len,
@@ -209,27 +210,37 @@ __device__ __forceinline__ void quad_chains(const uint8_t* __restrict__ arena,
   quad_addr(addr, line, i);
   uint64_t h0, h1;
   quad_init(i, h0, h1);
-  quad_run(h0, h1, 0, p, have ? L : 0u, have, true, lds, addr, line, i);
+  quad_run<kPrefetchAll>(h0, h1, 0, p, have ? L : 0u, have, true, lds, addr, line, i);
   if (have) *reinterpret_cast<uint64_t*>(out + (uint64_t)b * 32u + 8u * i) = h0;
 }
 
-__global__ __launch_bounds__(kThreads, 4) void k_mixed(const uint8_t* __restrict__ arena,
-                                                        const uint64_t* __restrict__ off,
-                                                        const uint32_t* __restrict__ len,
-                                                        const uint32_t* __restrict__ perm,
-                                                        uint64_t n, const uint32_t* n_long,
-                                                        uint32_t nq_wg, uint8_t* __restrict__ out) {
+// Quad part of an ordered batch: chains [0, nl), nl = min(*n_long, 64 nq_wg).
+// Latency-bound (one 1 MiB chain = 8192 dependent compressions), so it reads
+// each line's 48 message words up front (176 VGPRs) and runs at s_setprio 3;
+// it is its own kernel so the lane part keeps its occupancy.
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_quad_long(
+    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, const uint32_t* __restrict__ perm, const uint32_t* n_long,
+    uint32_t nq_wg, uint8_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWaves * kQuadWaveLds];
   const uint32_t nl = min(*n_long, nq_wg * 64u);
-  if (blockIdx.x < nq_wg) {
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t first = (blockIdx.x * kWaves + wave) * 16u;
-    if (first >= nl) return;
-    __builtin_amdgcn_s_setprio(3);
-    quad_chains(arena, off, len, perm, first, nl, out, lds, wave * kQuadWaveLds);
-    return;
-  }
-  const uint64_t j = nl + (uint64_t)(blockIdx.x - nq_wg) * kThreads + threadIdx.x;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t first = (blockIdx.x * kWaves + wave) * 16u;
+  if (first >= nl) return;
+  __builtin_amdgcn_s_setprio(3);
+  quad_chains<true>(arena, off, len, perm, first, nl, out, lds, wave * kQuadWaveLds);
+}
+
+// Lane part: chains [nl, n) of the order, one lane per chain.
+__global__ __launch_bounds__(kThreads, 4) void k_lane_rest(const uint8_t* __restrict__ arena,
+                                                            const uint64_t* __restrict__ off,
+                                                            const uint32_t* __restrict__ len,
+                                                            const uint32_t* __restrict__ perm,
+                                                            uint64_t n, const uint32_t* n_long,
+                                                            uint32_t nq_wg,
+                                                            uint8_t* __restrict__ out) {
+  const uint32_t nl = min(*n_long, nq_wg * 64u);
+  const uint64_t j = nl + (uint64_t)blockIdx.x * kThreads + threadIdx.x;
   if (j >= n) return;
   const uint32_t b = perm[j];
   uint64_t h[8];
@@ -415,14 +426,24 @@ hipError_t launch_general_desc(const uint8_t* arena, const uint64_t* off, const 
 
 hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
                         const uint32_t* perm, const uint32_t* n_long, uint64_t n, uint8_t* out,
-                        hipStream_t s) {
+                        hipStream_t s, hipStream_t aux, hipEvent_t fork, hipEvent_t join) {
   if (n == 0) return hipSuccess;
   const uint64_t nq = std::min<uint64_t>((n + 63) / 64, (uint64_t)kQuadMaxWg);
-  const uint64_t grid = nq + grid_for(n, kThreads);
-  if (grid > 0x7fffffffull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_mixed, dim3((unsigned)grid), dim3(kThreads), 0, s, arena, off, len, perm, n,
+  const uint64_t lane_grid = grid_for(n, kThreads);
+  if (lane_grid > 0x7fffffffull) return hipErrorInvalidValue;
+  hipError_t e = hipEventRecord(fork, s);
+  if (e == hipSuccess) e = hipStreamWaitEvent(aux, fork, 0);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads), 0, aux, arena, off,
+                     len, perm, n, n_long, (uint32_t)nq, out);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_quad_long, dim3((unsigned)nq), dim3(kThreads), 0, s, arena, off, len, perm,
                      n_long, (uint32_t)nq, out);
-  return hipGetLastError();
+  e = hipGetLastError();
+  if (e == hipSuccess) e = hipEventRecord(join, aux);
+  if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
+  return e;
 }
 
 hipError_t launch_fill_splitmix64(uint64_t* p, uint64_t nwords, uint64_t seed,

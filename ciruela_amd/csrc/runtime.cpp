@@ -55,6 +55,10 @@ Device::~Device() {
   if (order_free) (void)hipEventSynchronize(order_free);
   (void)hipFree(order_scratch);
   if (order_free) (void)hipEventDestroy(order_free);
+  if (aux) (void)hipStreamSynchronize(aux);
+  if (aux_fork) (void)hipEventDestroy(aux_fork);
+  if (aux_join) (void)hipEventDestroy(aux_join);
+  if (aux) (void)hipStreamDestroy(aux);
   if (compute) (void)hipStreamDestroy(compute);
   if (copy) (void)hipStreamDestroy(copy);
 }
@@ -123,7 +127,16 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
   if (n == 0) return CIR_OK;
   std::lock_guard<std::mutex> lk(d.order_mu);
   const size_t need = dev::order_scratch_bytes(n);
-  if (!d.order_free) CIR_HIP(hipEventCreateWithFlags(&d.order_free, hipEventDisableTiming));
+  if (!d.order_free) {  // created on d's device, whatever the caller's current one is
+    int cur = 0;
+    CIR_HIP(hipGetDevice(&cur));
+    CIR_HIP(hipSetDevice(d.id));
+    CIR_HIP(hipEventCreateWithFlags(&d.order_free, hipEventDisableTiming));
+    CIR_HIP(hipStreamCreateWithFlags(&d.aux, hipStreamNonBlocking));
+    CIR_HIP(hipEventCreateWithFlags(&d.aux_fork, hipEventDisableTiming));
+    CIR_HIP(hipEventCreateWithFlags(&d.aux_join, hipEventDisableTiming));
+    CIR_HIP(hipSetDevice(cur));
+  }
   if (need > d.order_cap) {
     CIR_HIP(hipEventSynchronize(d.order_free));
     (void)hipFree(d.order_scratch);
@@ -139,7 +152,8 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
   if (ht == CIR_HASH_SHA512_256)
     CIR_HIP(dev::launch_sha_desc(arena, off, len, perm, n, out, s));
   else
-    CIR_HIP(dev::launch_mixed(arena, off, len, perm, n_long, n, out, s));
+    CIR_HIP(dev::launch_mixed(arena, off, len, perm, n_long, n, out, s, d.aux, d.aux_fork,
+                              d.aux_join));
   CIR_HIP(hipEventRecord(d.order_free, s));
   return CIR_OK;
 }

@@ -63,6 +63,9 @@ struct Device {
   void* order_scratch = nullptr;
   size_t order_cap = 0;
   hipEvent_t order_free = nullptr;
+  // lane part of an ordered batch runs on `aux`, forked/joined by events
+  hipStream_t aux = nullptr;
+  hipEvent_t aux_fork = nullptr, aux_join = nullptr;
   // incremental footer chain (cir_scan_v1): own stream, state, text buffers
   std::mutex chain_mu;  // one incremental footer (scan) at a time per device
   hipStream_t chain = nullptr;

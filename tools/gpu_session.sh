@@ -45,6 +45,10 @@ for s in "$@"; do
       step hostreg 300 python tools/hostreg_probe.py > gpurun_out/hostreg.log 2>&1
       rm -f /dev/shm/hostreg_probe.bin
       cat gpurun_out/hostreg.log ;;
+    hostreg2)
+      step hostreg2 300 python tools/hostreg_probe2.py > gpurun_out/hostreg2.log 2>&1
+      rm -rf /dev/shm/hostreg2
+      cat gpurun_out/hostreg2.log ;;
     shadiag)
       step shadiag 300 python tools/sha_diag.py ;;
     cli)
