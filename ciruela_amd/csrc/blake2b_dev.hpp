@@ -126,9 +126,115 @@ __device__ __forceinline__ void compress_v(uint64_t h[8], const uint64_t m[16], 
   h[7] = xor3(h[7], v7, v15);
 }
 
+// ---------------------------------------------------------------------------
+// Step-major compression (the production form).  gfx950 issues the 32-bit
+// xor at 2 cycles per wave64 and the 64-bit add / funnel shift at 4
+// (tools/valu_ubench.hip); a stream that alternates the two classes issues
+// slower than the sum of its parts.  So each half-round runs one G step over
+// its 4 independent columns (or diagonals) at a time, and a scheduling
+// barrier at every change of class keeps the compiler from re-interleaving:
+// 8 slow | 8 fast | 4 slow | 8 fast | 16 slow | 8 fast | 12 slow | 8 fast |
+// 8 slow.  Same instructions as compress_v; 4 % faster register-only
+// (tools/order_ubench.hip).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
+
+template <int N>
+__device__ __forceinline__ uint64_t rotr_lh(uint32_t l, uint32_t h) {
+  if constexpr (N == 32)
+    return mk64(h, l);
+  else if constexpr (N < 32)
+    return mk64(__builtin_amdgcn_alignbit(h, l, N), __builtin_amdgcn_alignbit(l, h, N));
+  else
+    return mk64(__builtin_amdgcn_alignbit(l, h, N - 32), __builtin_amdgcn_alignbit(h, l, N - 32));
+}
+
+#define CIR_XOR4(P, Q)                                            \
+  tl0 = lo32(P##0) ^ lo32(Q##0); th0 = hi32(P##0) ^ hi32(Q##0);  \
+  tl1 = lo32(P##1) ^ lo32(Q##1); th1 = hi32(P##1) ^ hi32(Q##1);  \
+  tl2 = lo32(P##2) ^ lo32(Q##2); th2 = hi32(P##2) ^ hi32(Q##2);  \
+  tl3 = lo32(P##3) ^ lo32(Q##3); th3 = hi32(P##3) ^ hi32(Q##3);
+#define CIR_ROT4(P, N)              \
+  P##0 = rotr_lh<N>(tl0, th0);      \
+  P##1 = rotr_lh<N>(tl1, th1);      \
+  P##2 = rotr_lh<N>(tl2, th2);      \
+  P##3 = rotr_lh<N>(tl3, th3);
+#define CIR_ADD4(P, Q) P##0 = P##0 + (Q##0); P##1 = P##1 + (Q##1); P##2 = P##2 + (Q##2); P##3 = P##3 + (Q##3);
+
+// 4 independent G: (a_k, b_k, c_k, d_k) with messages x_k, y_k.
+__device__ __forceinline__ void g4(uint64_t& a0, uint64_t& a1, uint64_t& a2, uint64_t& a3,
+                                   uint64_t& b0, uint64_t& b1, uint64_t& b2, uint64_t& b3,
+                                   uint64_t& c0, uint64_t& c1, uint64_t& c2, uint64_t& c3,
+                                   uint64_t& d0, uint64_t& d1, uint64_t& d2, uint64_t& d3,
+                                   uint64_t x0, uint64_t x1, uint64_t x2, uint64_t x3,
+                                   uint64_t y0, uint64_t y1, uint64_t y2, uint64_t y3) {
+  uint32_t tl0, tl1, tl2, tl3, th0, th1, th2, th3;
+  CIR_ADD4(a, x) CIR_ADD4(a, b)            // slow
+  sched_fence();
+  CIR_XOR4(d, a) CIR_ROT4(d, 32)          // fast (rotr 32 is a register swap)
+  sched_fence();
+  CIR_ADD4(c, d)                          // slow
+  sched_fence();
+  CIR_XOR4(b, c)                          // fast
+  sched_fence();
+  CIR_ROT4(b, 24) CIR_ADD4(a, y) CIR_ADD4(a, b)  // slow
+  sched_fence();
+  CIR_XOR4(d, a)                          // fast
+  sched_fence();
+  CIR_ROT4(d, 16) CIR_ADD4(c, d)          // slow
+  sched_fence();
+  CIR_XOR4(b, c)                          // fast
+  sched_fence();
+  CIR_ROT4(b, 63)                         // slow (runs on into the next g4's adds)
+}
+
+#define CIR_ROUND_SM(s0, s1, s2, s3, s4, s5, s6, s7, s8, s9, s10, s11, s12, s13, s14, s15)    \
+  g4(v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12, v13, v14, v15, m[s0], m[s2], m[s4], \
+     m[s6], m[s1], m[s3], m[s5], m[s7]);                                                       \
+  g4(v0, v1, v2, v3, v5, v6, v7, v4, v10, v11, v8, v9, v15, v12, v13, v14, m[s8], m[s10],       \
+     m[s12], m[s14], m[s9], m[s11], m[s13], m[s15]);
+
+__device__ __forceinline__ void compress_sm(uint64_t h[8], const uint64_t m[16], uint64_t t,
+                                            bool last) {
+  uint64_t v0 = h[0], v1 = h[1], v2 = h[2], v3 = h[3];
+  uint64_t v4 = h[4], v5 = h[5], v6 = h[6], v7 = h[7];
+  uint64_t v8 = CIR_IV0, v9 = CIR_IV1, v10 = CIR_IV2, v11 = CIR_IV3;
+  uint64_t v12 = CIR_IV4 ^ t, v13 = CIR_IV5;
+  uint64_t v14 = last ? ~CIR_IV6 : CIR_IV6, v15 = CIR_IV7;
+  CIR_ROUND_SM(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
+  CIR_ROUND_SM(14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3)
+  CIR_ROUND_SM(11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4)
+  CIR_ROUND_SM(7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8)
+  CIR_ROUND_SM(9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13)
+  CIR_ROUND_SM(2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9)
+  CIR_ROUND_SM(12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11)
+  CIR_ROUND_SM(13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10)
+  CIR_ROUND_SM(6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5)
+  CIR_ROUND_SM(10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0)
+  CIR_ROUND_SM(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
+  CIR_ROUND_SM(14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3)
+  sched_fence();
+  h[0] = xor3(h[0], v0, v8);
+  h[1] = xor3(h[1], v1, v9);
+  h[2] = xor3(h[2], v2, v10);
+  h[3] = xor3(h[3], v3, v11);
+  h[4] = xor3(h[4], v4, v12);
+  h[5] = xor3(h[5], v5, v13);
+  h[6] = xor3(h[6], v6, v14);
+  h[7] = xor3(h[7], v7, v15);
+}
+
+#ifndef CIR_COMPRESS_SM
+#define CIR_COMPRESS_SM 1
+#endif
+
 __device__ __forceinline__ void compress(uint64_t h[8], const uint64_t m[16], uint64_t t,
                                          bool last) {
+#if CIR_COMPRESS_SM
+  compress_sm(h, m, t, last);
+#else
   compress_v<0, 0, 0>(h, m, t, last);
+#endif
 }
 
 // Two independent chains interleaved (ILP 8); same rounds as compress_v.
@@ -236,10 +342,15 @@ __device__ __forceinline__ void load_line_safe(uint64_t m[16], const uint8_t* p,
 __device__ __forceinline__ void load_line_any(uint64_t m[16], const uint8_t* p, uint64_t i,
                                               uint64_t nfull, uint32_t rem, bool al16) {
   const uint8_t* q = p + (i << 7);
-  if (al16 && i < nfull)
+  if (al16 && i < nfull) {
     load_line16(m, q);
-  else
-    load_line_safe(m, q, i < nfull ? 128u : rem);
+  } else {
+    // opaque: keeps the 128 byte-position compares inside the loop (hoisted,
+    // they would occupy SGPR masks and spill)
+    uint32_t n = i < nfull ? 128u : rem;
+    asm volatile("" : "+v"(n));
+    load_line_safe(m, q, n);
+  }
 }
 
 // Digest of one chain (a block of len bytes at p) into h[0..3].

@@ -303,7 +303,7 @@ hipError_t launch_sha_desc(const uint8_t* arena, const uint64_t* off, const uint
 // Register-only compressions (no memory traffic): `lines` compressions per
 // lane on a message kept in registers -- the measured VALU ceiling the bench
 // reports next to the HBM roofline (diagnostics, not part of the reference).
-__global__ __launch_bounds__(kThreads, 5) void k_compress_only(uint8_t* __restrict__ out,
+__global__ __launch_bounds__(kThreads, 4) void k_compress_only(uint8_t* __restrict__ out,
                                                               uint32_t lines) {
   const uint64_t b = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
   uint64_t h[8], m[16];

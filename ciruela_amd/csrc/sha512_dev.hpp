@@ -148,16 +148,22 @@ __device__ __forceinline__ uint64_t bswap64(uint64_t x) {
 // one compression; w = the 16 message words, big-endian decoded
 __device__ __forceinline__ void compress(uint64_t h[8], uint64_t w[16]) {
   uint64_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+  // 5 x 16 rounds: the message-schedule indices stay static inside the
+  // unrolled 16, and the round constants are scalar loads per pass (a full
+  // unroll hoists all 160 constant dwords into SGPRs and spills).
+#pragma unroll 1
+  for (int t0 = 0; t0 < 80; t0 += 16) {
 #pragma unroll
-  for (int t = 0; t < 80; ++t) {
-    if (t >= 16) {
-      const uint64_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
+  for (int i = 0; i < 16; ++i) {
+    const int t = t0 + i;
+    if (t0 > 0) {
+      const uint64_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
       const uint64_t s0 = x3(rotr<1>(w15), rotr<8>(w15), shr<7>(w15));
       const uint64_t s1 = x3(rotr<19>(w2), rotr<61>(w2), shr<6>(w2));
-      w[t & 15] = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+      w[i] = w[i] + s0 + w[(i + 9) & 15] + s1;
     }
     const uint64_t t1 = hh + x3(rotr<14>(e), rotr<18>(e), rotr<41>(e)) + ch(e, f, g) + kK[t] +
-                        w[t & 15];
+                        w[i];
     const uint64_t t2 = x3(rotr<28>(a), rotr<34>(a), rotr<39>(a)) + maj(a, b, c);
     hh = g;
     g = f;
@@ -167,6 +173,7 @@ __device__ __forceinline__ void compress(uint64_t h[8], uint64_t w[16]) {
     c = b;
     b = a;
     a = t1 + t2;
+  }
   }
   h[0] += a;
   h[1] += b;
@@ -226,7 +233,12 @@ __device__ __forceinline__ void chain(const uint8_t* p, uint64_t len, uint64_t h
       else
         load_block_padded(m, q, 128u, false);
     } else if (bi == pad_blk) {
-      load_block_padded(m, q, tail, true);
+      // opaque here: the 128 byte-position compares against the tail length
+      // must not be hoisted out of the block loop (they would live in SGPR
+      // masks and spill)
+      uint32_t tn = tail;
+      asm volatile("" : "+v"(tn));
+      load_block_padded(m, q, tn, true);
     } else {
 #pragma unroll
       for (int k = 0; k < 16; ++k) m[k] = 0;

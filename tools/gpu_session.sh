@@ -107,6 +107,9 @@ for s in "$@"; do
         --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 1 --steps 5 --warmup 1 --force-dist \
         --no-cpu-baseline > gpurun_out/dist1.json 2> gpurun_out/dist1.err
       cat gpurun_out/dist1.json ;;
+    order)
+      step order 300 ./build/order_ubench > gpurun_out/order.log 2>&1
+      cat gpurun_out/order.log ;;
     ubench)
       step ubench 300 ./build/valu_ubench > gpurun_out/ubench.log 2>&1
       cat gpurun_out/ubench.log ;;
