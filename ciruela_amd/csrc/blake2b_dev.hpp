@@ -30,6 +30,13 @@ __device__ __forceinline__ uint32_t hi32(uint64_t x) { return (uint32_t)(x >> 32
 __device__ __forceinline__ uint64_t mk64(uint32_t lo, uint32_t hi) {
   return ((uint64_t)hi << 32) | lo;
 }
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+// Same value as mk64, built as a 2-vector: an add of it stays one 64-bit add
+// of a register pair (the shift/or form gets re-associated into two adds).
+__device__ __forceinline__ uint64_t mk64_pair(uint32_t lo, uint32_t hi) {
+  const u32x2_t v = {lo, hi};
+  return __builtin_bit_cast(uint64_t, v);
+}
 
 // rotr64(a ^ b, N) on 32-bit halves.  MODE selects the instruction form
 // (gfx950 issue costs measured by tools/valu_ubench.hip, profiles/):
@@ -384,6 +391,14 @@ __device__ __forceinline__ void hash_chain(const uint8_t* p, uint64_t len, uint6
 // per compression per lane instead of ~2000: a chain finishes ~2.8x sooner,
 // at ~1.4x the total instruction count of lane-per-chain mode.
 // ---------------------------------------------------------------------------
+// DPP quad_perm read of another lane's 32-bit value.  update_dpp with a zero
+// "old" lets the compiler fold the permute into the consuming VOP2
+// instruction (v_xor_b32_dpp) instead of emitting a v_mov_b32_dpp.
+template <int CTRL>
+__device__ __forceinline__ uint32_t qd(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
+}
+// Whole 64-bit value into registers (v_mov_b32_dpp x2; no "old" operand).
 template <int CTRL>
 __device__ __forceinline__ uint64_t qperm(uint64_t x) {
   return mk64((uint32_t)__builtin_amdgcn_mov_dpp((int)lo32(x), CTRL, 0xf, 0xf, false),
@@ -393,24 +408,51 @@ constexpr int kQuadFromNext = 0x39;   // lane i <- lane i+1  (quad_perm [1,2,3,0
 constexpr int kQuadFromNext2 = 0x4E;  // lane i <- lane i+2  (quad_perm [2,3,0,1])
 constexpr int kQuadFromPrev = 0x93;   // lane i <- lane i+3  (quad_perm [3,0,1,2])
 
-// (a + m) + b: the message add does not wait for b, so only one 64-bit add
-// per half-G sits on the chain's critical path (quad mode is latency-bound).
-#define CIR_GQ(x, y)                  \
-  a = (a + (x)) + b;                  \
-  d = xor_rotr<32, 0>(d, a);          \
-  c = c + d;                          \
-  b = xor_rotr<24, 0>(b, c);          \
-  a = (a + (y)) + b;                  \
-  d = xor_rotr<16, 0>(d, a);          \
-  c = c + d;                          \
+// One G of quad mode.  The state arrives in the layout of the previous half
+// round; PB / PC / PD (0 = own lane) name the lanes b, c, d are read from,
+// so the column <-> diagonal moves happen inside this G: b and c are
+// permuted into registers (both feed 64-bit adds, which have no DPP form),
+// d is permuted inside its first consumer, the xor of the rotr-32 step.
+// (a + m) + b: the message add does not wait for b.
+template <int PB, int PC, int PD>
+__device__ __forceinline__ void g_quad(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d,
+                                       uint64_t x, uint64_t y) {
+  a = a + x;
+  if constexpr (PB != 0) b = qperm<PB>(b);
+  if constexpr (PC != 0) c = qperm<PC>(c);
+  a = a + b;
+  uint32_t dl, dh;  // rotr32(d ^ a): swap the halves
+  if constexpr (PD != 0) {
+    dl = qd<PD>(hi32(d)) ^ hi32(a);
+    dh = qd<PD>(lo32(d)) ^ lo32(a);
+  } else {
+    dl = hi32(d) ^ hi32(a);
+    dh = lo32(d) ^ lo32(a);
+  }
+  d = mk64(dl, dh);
+  c = c + d;
+  b = xor_rotr<24, 0>(b, c);
+  a = (a + y) + b;
+  {
+    // the rotate's halves built as a vector, not (hi << 32) | lo: the
+    // compiler then keeps them as one register pair instead of adding them
+    // into c separately (an extra 64-bit add and a move per G)
+    const uint32_t l = lo32(d) ^ lo32(a), h = hi32(d) ^ hi32(a);
+    d = mk64_pair(__builtin_amdgcn_alignbit(h, l, 16), __builtin_amdgcn_alignbit(l, h, 16));
+  }
+  c = c + d;
   b = xor_rotr<63, 0>(b, c);
+}
 
 // One compression of the chain owned by this quad.  line = the quad's 128-B
 // message line in LDS; addr[r*4 + k] = byte offset of the k-th word lane i
 // needs in round r.  cv/dv = IV[i]/IV[4+i]; dmask = this lane's t / final-flag
 // contribution to v[12+i].  kPrefetchAll: issue all 48 LDS reads before the
-// first round (+96 VGPRs) so no round waits on LDS latency -- for the
-// single-chain footer kernel, whose one wave has registers to spare.
+// first round (+96 VGPRs) so no round waits on LDS latency.
+// A quad's single wave issues ~1 VALU instruction per 4.3-5 cycles whether
+// or not it depends on the previous one (tools/lat_ubench.hip), so the
+// latency of a chain is its instruction count: 20 per G + 4 permutes per
+// layout change, the finalisation reading c, b, d across lanes.
 template <bool kPrefetchAll>
 __device__ __forceinline__ void compress_quad_t(uint64_t& h0, uint64_t& h1, const uint8_t* line,
                                                 const uint32_t (&addr)[48], uint64_t cv,
@@ -431,23 +473,21 @@ __device__ __forceinline__ void compress_quad_t(uint64_t& h0, uint64_t& h1, cons
     else
       return *reinterpret_cast<const uint64_t*>(line + addr[k]);
   };
+  g_quad<0, 0, 0>(a, b, c, d, word(0), word(1));
+  g_quad<kQuadFromNext, kQuadFromNext2, kQuadFromPrev>(a, b, c, d, word(2), word(3));
 #pragma unroll
-  for (int r = 0; r < 12; ++r) {
-    const uint64_t x0 = word(4 * r + 0);
-    const uint64_t y0 = word(4 * r + 1);
-    CIR_GQ(x0, y0)
-    b = qperm<kQuadFromNext>(b);
-    c = qperm<kQuadFromNext2>(c);
-    d = qperm<kQuadFromPrev>(d);
-    const uint64_t x1 = word(4 * r + 2);
-    const uint64_t y1 = word(4 * r + 3);
-    CIR_GQ(x1, y1)
-    b = qperm<kQuadFromPrev>(b);
-    c = qperm<kQuadFromNext2>(c);
-    d = qperm<kQuadFromNext>(d);
+  for (int r = 1; r < 12; ++r) {
+    g_quad<kQuadFromPrev, kQuadFromNext2, kQuadFromNext>(a, b, c, d, word(4 * r + 0),
+                                                         word(4 * r + 1));
+    g_quad<kQuadFromNext, kQuadFromNext2, kQuadFromPrev>(a, b, c, d, word(4 * r + 2),
+                                                         word(4 * r + 3));
   }
-  h0 = xor3(h0, a, c);
-  h1 = xor3(h1, b, d);
+  // back to the column layout inside the finalisation: c_i from lane i+2,
+  // b_i from lane i+3, d_i from lane i+1
+  const uint64_t cc = mk64(qd<kQuadFromNext2>(lo32(c)) ^ lo32(a), qd<kQuadFromNext2>(hi32(c)) ^ hi32(a));
+  h0 = h0 ^ cc;
+  const uint64_t bb = mk64(qd<kQuadFromPrev>(lo32(b)) ^ lo32(h1), qd<kQuadFromPrev>(hi32(b)) ^ hi32(h1));
+  h1 = mk64(qd<kQuadFromNext>(lo32(d)) ^ lo32(bb), qd<kQuadFromNext>(hi32(d)) ^ hi32(bb));
 }
 
 __device__ __forceinline__ void compress_quad(uint64_t& h0, uint64_t& h1, const uint8_t* line,

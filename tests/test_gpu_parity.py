@@ -424,3 +424,49 @@ def test_check_file_commit(gpu, small_ctx, tmp_path):
     empty.write_bytes(b"")
     with open(empty, "rb") as f:
         assert gpu.Hashes(b"", 32768).check_file(f, context=small_ctx)
+
+
+def test_desc_quad_mode_edges(gpu, ctx, oracle):
+    """Chains around the quad-mode threshold (2048 lines = 256 KiB) and long
+    ragged chains: 37 long chains (a partial 16-chain wave), misaligned and
+    128-aligned starts, final lines of 1..127 bytes, next to short chains
+    that share the launch (k_quad_long + k_lane_rest)."""
+    import torch
+    q = 2048 * 128
+    rng = random.Random(0x9A4D)
+    lens = [q - 1, q, q + 1, q + 127, q + 128, q + 129, 1 << 20, (1 << 20) + 5, (3 << 20) + 77]
+    lens += [rng.randrange(q, 2 << 20) for _ in range(28)]
+    lens += [rng.choice([0, 1, 128, 4096, 32768, rng.randrange(1, 70000)]) for _ in range(500)]
+    rng.shuffle(lens)
+    offs, pos = [], 0
+    for i, ln in enumerate(lens):
+        pos += (-pos) % 16 + (i % 5)
+        offs.append(pos)
+        pos += ln
+    data = dev_random(gpu, pos, seed=17)
+    d_off = torch.tensor(offs, dtype=torch.int64, device="cuda:0")
+    d_len = torch.tensor(lens, dtype=torch.int32, device="cuda:0")
+    out = torch.zeros(32 * len(lens), dtype=torch.uint8, device="cuda:0")
+    ctx.hash_blocks_dev(data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), len(lens),
+                        out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    host = data.cpu().numpy()
+    want = np.zeros(32 * len(lens), dtype=np.uint8)
+    ao = np.array(offs, dtype=np.uint64)  # kept alive across the call
+    al = np.array(lens, dtype=np.uint32)
+    oracle.oracle_hash_blocks(host.ctypes.data, ao.ctypes.data, al.ctypes.data, len(lens),
+                              want.ctypes.data, 8)
+    assert first_bad(out.cpu().numpy(), want) is None
+
+
+def test_scan_long_index_footer(gpu, small_ctx, tmp_path):
+    """An index body of several MiB (128-byte blocks): the footer chain is fed
+    to the device in >= 1 MiB pieces while later batches hash (scan.cpp
+    FooterChain) and must still equal H(body) (src/index.rs:98-105)."""
+    rng = random.Random(5)
+    for k in range(6):
+        (tmp_path / ("f%d.bin" % k)).write_bytes(rng.randbytes(rng.randrange(1 << 20, 3 << 20)))
+    cfg = gpu.ScannerConfig.new().block_size(128).add_dir(str(tmp_path), "/")
+    got = gpu.v1.scan(cfg, context=small_ctx)
+    assert len(got) > (4 << 20)
+    assert got == dirsig_oracle.scan(str(tmp_path), 128)

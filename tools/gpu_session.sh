@@ -107,6 +107,12 @@ for s in "$@"; do
         --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 1 --steps 5 --warmup 1 --force-dist \
         --no-cpu-baseline > gpurun_out/dist1.json 2> gpurun_out/dist1.err
       cat gpurun_out/dist1.json ;;
+    quad)
+      step quad 300 python tools/quad_probe.py > gpurun_out/quad.log 2>&1
+      cat gpurun_out/quad.log ;;
+    lat)
+      step lat 300 ./build/lat_ubench > gpurun_out/lat.log 2>&1
+      cat gpurun_out/lat.log ;;
     order)
       step order 300 ./build/order_ubench > gpurun_out/order.log 2>&1
       cat gpurun_out/order.log ;;
