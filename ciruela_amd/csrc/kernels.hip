@@ -41,7 +41,10 @@ __global__ __launch_bounds__(kThreads, 5) void k_uniform_glds(const uint8_t* __r
 // loader, the others hash blocks [0, nuni) 64 per wave through LDS.  The
 // ragged workgroups come first so their chains start with the rest instead
 // of trailing the launch.
-__global__ __launch_bounds__(kThreads, 5) void k_chunks(const uint8_t* __restrict__ data,
+#ifndef CIR_UNI_OCC
+#define CIR_UNI_OCC 5
+#endif
+__global__ __launch_bounds__(kThreads, CIR_UNI_OCC) void k_chunks(const uint8_t* __restrict__ data,
                                                          uint64_t nbytes, uint64_t bs,
                                                          uint32_t lines, uint64_t nuni,
                                                          uint64_t nblk, uint32_t ngen_wg,

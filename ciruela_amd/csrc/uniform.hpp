@@ -10,6 +10,12 @@ namespace dev {
 
 constexpr int kWaves = kThreads / 64;
 
+// cache-policy bits of the LDS-DMA loads: 2 = nt (streamed, read once;
+// MI355X_MICROARCH.md nt-weights).  A/B in-process: within 1 % of 0.
+#ifndef CIR_DMA_AUX
+#define CIR_DMA_AUX 2
+#endif
+
 // ---------------------------------------------------------------------------
 // LDS image of one wave's message lines (8 KiB, no padding).
 // DMA instruction j (0..7) fills bytes [1024 j, 1024 j + 1024): lane l
@@ -48,7 +54,7 @@ __device__ __forceinline__ void uniform_glds_wave(const uint8_t* __restrict__ ws
       const uint8_t* src = line + (uint64_t)j * jstride + (dma_lane ^ (16u * j));
       __builtin_amdgcn_global_load_lds(
           (const void __attribute__((address_space(1)))*)src,
-          (void __attribute__((address_space(3)))*)(wl + j * 1024), 16, 0, 0);
+          (void __attribute__((address_space(3)))*)(wl + j * 1024), 16, 0, CIR_DMA_AUX);
     }
   };
 

@@ -107,6 +107,9 @@ for s in "$@"; do
         --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 1 --steps 5 --warmup 1 --force-dist \
         --no-cpu-baseline > gpurun_out/dist1.json 2> gpurun_out/dist1.err
       cat gpurun_out/dist1.json ;;
+    dvfs)
+      step dvfs 300 ./build/dvfs_probe > gpurun_out/dvfs.log 2>&1
+      cat gpurun_out/dvfs.log ;;
     quad)
       step quad 300 python tools/quad_probe.py > gpurun_out/quad.log 2>&1
       cat gpurun_out/quad.log ;;
