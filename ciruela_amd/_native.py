@@ -17,7 +17,8 @@ except Exception:  # pragma: no cover - torch is optional for the library
     _torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libciruela_amd.so")
+# CIRUELA_AMD_LIB: another build of the same library (A/B of build variants)
+LIB_PATH = os.environ.get("CIRUELA_AMD_LIB") or os.path.join(_HERE, "libciruela_amd.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(

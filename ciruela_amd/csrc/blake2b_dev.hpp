@@ -458,18 +458,20 @@ __device__ __forceinline__ void compress_quad_t(uint64_t& h0, uint64_t& h1, cons
                                                 const uint32_t (&addr)[48], uint64_t cv,
                                                 uint64_t dv) {
   uint64_t a = h0, b = h1, c = cv, d = dv;
-  uint64_t msg[kPrefetchAll ? 48 : 1];
+  // rounds 10 and 11 repeat the schedules of rounds 0 and 1: 40 distinct
+  // (round, position) words per lane
+  uint64_t msg[kPrefetchAll ? 40 : 1];
   if constexpr (kPrefetchAll) {
 #pragma unroll
-    for (int k = 0; k < 48; ++k) msg[k] = *reinterpret_cast<const uint64_t*>(line + addr[k]);
+    for (int k = 0; k < 40; ++k) msg[k] = *reinterpret_cast<const uint64_t*>(line + addr[k]);
     // consume every word here: the scheduler cannot sink the reads back into
     // the rounds, so the compression waits on LDS once instead of per round
 #pragma unroll
-    for (int k = 0; k < 48; ++k) asm volatile("" : "+v"(msg[k]));
+    for (int k = 0; k < 40; ++k) asm volatile("" : "+v"(msg[k]));
   }
   auto word = [&](int k) -> uint64_t {
     if constexpr (kPrefetchAll)
-      return msg[k];
+      return msg[k < 40 ? k : k - 40];
     else
       return *reinterpret_cast<const uint64_t*>(line + addr[k]);
   };

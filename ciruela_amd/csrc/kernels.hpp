@@ -10,8 +10,14 @@ constexpr int kThreads = 256;  // 4 waves per workgroup
 
 enum class Loader : int { kGlds = 0, kDirect = 1 };
 
-// Chains of at least this many 128-B lines (256 KiB) run 4 lanes per chain.
-constexpr uint32_t kQuadMinLines = 2048;
+// Chains of at least this many 128-B lines (128 KiB) run 4 lanes per chain.
+// config 3 A/B (profiles/r01/cfg3_quad_threshold.log): 2048 lines 659 GiB/s,
+// 1024 782, 512 760, 256 769 -- below 2048, the ragged 1 MiB blocks no
+// longer trail the lane kernel.
+#ifndef CIR_QUAD_MIN_LINES
+#define CIR_QUAD_MIN_LINES 1024
+#endif
+constexpr uint32_t kQuadMinLines = CIR_QUAD_MIN_LINES;
 constexpr int kQuadMaxWg = 256;  // at most 256 x 64 = 16384 chains in quad mode
 
 // nblk equal blocks of bs bytes at data (bs % 128 == 0, data 16-byte aligned,

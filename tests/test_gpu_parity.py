@@ -427,15 +427,16 @@ def test_check_file_commit(gpu, small_ctx, tmp_path):
 
 
 def test_desc_quad_mode_edges(gpu, ctx, oracle):
-    """Chains around the quad-mode threshold (2048 lines = 256 KiB) and long
+    """Chains around the quad-mode threshold (1024 lines = 128 KiB) and long
     ragged chains: 37 long chains (a partial 16-chain wave), misaligned and
     128-aligned starts, final lines of 1..127 bytes, next to short chains
     that share the launch (k_quad_long + k_lane_rest)."""
     import torch
-    q = 2048 * 128
+    q = 1024 * 128  # kQuadMinLines (kernels.hpp)
     rng = random.Random(0x9A4D)
-    lens = [q - 1, q, q + 1, q + 127, q + 128, q + 129, 1 << 20, (1 << 20) + 5, (3 << 20) + 77]
-    lens += [rng.randrange(q, 2 << 20) for _ in range(28)]
+    lens = [q - 1, q, q + 1, q + 127, q + 128, q + 129, 2 * q - 1, 2 * q, 2 * q + 1,
+            1 << 20, (1 << 20) + 5, (3 << 20) + 77]
+    lens += [rng.randrange(q, 2 << 20) for _ in range(25)]
     lens += [rng.choice([0, 1, 128, 4096, 32768, rng.randrange(1, 70000)]) for _ in range(500)]
     rng.shuffle(lens)
     offs, pos = [], 0

@@ -84,6 +84,17 @@ for s in "$@"; do
       step cfg3 600 python bench.py --workload config3 --steps 5 --warmup 1 \
         > gpurun_out/cfg3.json 2> gpurun_out/cfg3.err
       cat gpurun_out/cfg3.json ;;
+    prof3)
+      step prof3 600 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d gpurun_out/prof3 -o run -- python3 bench.py --workload config3 --steps 3 --warmup 1 \
+        > gpurun_out/prof3.log 2>&1
+      cat gpurun_out/prof3/run_kernel_stats.csv | cut -c1-200 ;;
+    cfg3ab)
+      for lib in abtest/*.so; do
+        CIRUELA_AMD_LIB=$PWD/$lib step "cfg3_$lib" 300 python bench.py --workload config3 --steps 5 --warmup 1 \
+          > gpurun_out/cfg3ab.json 2> gpurun_out/cfg3ab.err
+        echo "$lib $(cat gpurun_out/cfg3ab.json)"
+      done ;;
     cfg1)
       step cfg1 300 python bench.py --workload config1 > gpurun_out/cfg1.json 2> gpurun_out/cfg1.err
       cat gpurun_out/cfg1.json ;;
