@@ -471,3 +471,54 @@ def test_scan_long_index_footer(gpu, small_ctx, tmp_path):
     got = gpu.v1.scan(cfg, context=small_ctx)
     assert len(got) > (4 << 20)
     assert got == dirsig_oracle.scan(str(tmp_path), 128)
+
+
+def test_concurrent_callers_one_context(gpu, small_ctx, oracle):
+    """The ABI is callable from several host threads at once on one context
+    (the scan's worker threads, the daemon's fetch and commit tasks): host
+    batches, in-memory files and device batches on distinct streams."""
+    import threading
+
+    import torch
+    rng = random.Random(77)
+    arena = rng.randbytes(3 << 20)
+    jobs, errors = [], []
+
+    def host_blocks(seed):
+        r = random.Random(seed)
+        lens = [r.choice([0, 1, 4096, 32768, r.randrange(1, 300000)]) for _ in range(300)]
+        offs = [r.randrange(0, len(arena) - ln + 1) for ln in lens]
+        got = small_ctx.hash_blocks(arena, offs, lens)
+        for i in range(len(lens)):
+            if got[32 * i:32 * i + 32] != oracle_digest(oracle, arena[offs[i]:offs[i] + lens[i]]):
+                errors.append(("blocks", seed, i))
+                return
+
+    def device_blocks(seed):
+        r = random.Random(seed)
+        lens = [r.choice([128, 32768, 200000, r.randrange(1, 70000)]) for _ in range(200)]
+        offs = [r.randrange(0, len(arena) - ln + 1) for ln in lens]
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            data = torch.frombuffer(bytearray(arena), dtype=torch.uint8).to("cuda:0")
+            d_off = torch.tensor(offs, dtype=torch.int64, device="cuda:0")
+            d_len = torch.tensor(lens, dtype=torch.int32, device="cuda:0")
+            out = torch.zeros(32 * len(lens), dtype=torch.uint8, device="cuda:0")
+        small_ctx.hash_blocks_dev(data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), len(lens),
+                                  out.data_ptr(), s.cuda_stream)
+        s.synchronize()
+        got = out.cpu().numpy().tobytes()
+        for i in range(len(lens)):
+            if got[32 * i:32 * i + 32] != oracle_digest(oracle, arena[offs[i]:offs[i] + lens[i]]):
+                errors.append(("device", seed, i))
+                return
+
+    for k in range(4):
+        jobs.append(threading.Thread(target=host_blocks, args=(k,)))
+        jobs.append(threading.Thread(target=device_blocks, args=(100 + k,)))
+    for t in jobs:
+        t.start()
+    for t in jobs:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in jobs)
+    assert errors == []
