@@ -53,9 +53,10 @@ def parse():
     p.add_argument("--block-size", type=int, default=32768)
     p.add_argument("--loader", choices=["glds", "direct", "api"], default="api",
                    help="api = cir_hash_chunks_dev (production path, LDS-DMA loader)")
-    p.add_argument("--workload", choices=["auto", "config3", "config5", "config1"],
+    p.add_argument("--workload", choices=["auto", "config3", "config5", "config1", "config2host"],
                    default="auto", help="auto = config2 at N=1, config4 at N>1")
     p.add_argument("--tree-gib", type=float, default=50.0, help="config5 tree size")
+    p.add_argument("--host-gib", type=int, default=32, help="config2host buffer size")
     p.add_argument("--tree-dir", default="/dev/shm/ciruela_bench_tree")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--force-dist", action="store_true",
@@ -203,6 +204,41 @@ def run_config3(args, ca, ctx, dev, stream):
             "note": "includes the on-device longest-chain-first sort (order.hip)"}
 
 
+def run_config2host(args, ca, ctx, dev, stream):
+    """Config 2's blocks handed over in (pageable) host memory: cir_hash_memory
+    = Hashes::hash_file over an in-memory file, digests back in host memory.
+    The PCIe-inclusive rate of the headline shape; never `value`
+    of the headline line."""
+    import numpy as np
+    import torch
+    bs = args.block_size
+    nbytes = args.host_gib << 30
+    data = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    fill_config2(ca, data, bs, stream)
+    dev_out = torch.empty(nbytes // bs * 32, dtype=torch.uint8, device=dev)
+    ca._n.check(ca._n.lib.cir_hash_chunks_dev(ctx.handle, data.data_ptr(), nbytes, bs,
+                                              dev_out.data_ptr(), stream))
+    torch.cuda.synchronize()
+    want = dev_out.cpu().numpy().tobytes()
+    host = np.empty(nbytes, dtype=np.uint8)
+    torch.from_numpy(host).copy_(data)  # pageable host copy of the same bytes
+    del data, dev_out
+    torch.cuda.empty_cache()
+    times = []
+    for _ in range(max(1, args.steps)):
+        t0 = time.perf_counter()
+        got = ctx.hash_memory(host, bs)
+        times.append(time.perf_counter() - t0)
+    best = min(times)
+    return {"metric": "GiB/s block-hashed from host memory, config 2 shape (PCIe-inclusive)",
+            "value": round(nbytes / best / GIB, 3), "unit": "GiB/s",
+            "seconds_best": round(best, 3), "seconds_all": [round(t, 3) for t in times],
+            "bytes": nbytes, "block_size": bs, "entry_point": "cir_hash_memory",
+            "matches_device_resident": got == want,
+            "note": "pageable host buffer -> pinned staging (16 copy threads) -> H2D -> "
+                    "k_chunks -> D2H digests, double-buffered"}
+
+
 def make_tree(root, gib, file_mib=32, ndirs=40, seed=0x5EED0005):
     """Config 5 tree: files of file_mib MiB in ndirs directories."""
     import numpy as np
@@ -305,7 +341,8 @@ def main():
             raise SystemExit("secondary workloads run on one GPU")
         rec = {"config3": lambda: run_config3(args, ca, ctx, dev, stream),
                "config5": lambda: run_config5(args, ca, ctx),
-               "config1": lambda: run_config1(args, ca, ctx)}[args.workload]()
+               "config1": lambda: run_config1(args, ca, ctx),
+               "config2host": lambda: run_config2host(args, ca, ctx, dev, stream)}[args.workload]()
         print(json.dumps(rec), flush=True)
         return 0
 

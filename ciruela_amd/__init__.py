@@ -39,18 +39,20 @@ DEFAULT_BLOCK_SIZE = 32768
 
 
 def _buf(data):
-    """(pointer, keepalive) for a bytes-like object."""
-    if isinstance(data, (bytes, bytearray, memoryview)):
-        mv = memoryview(data).cast("B")
-        n = mv.nbytes
-        if n == 0:
-            return None, b""
-        if mv.readonly:
-            arr = (ctypes.c_char * n).from_buffer_copy(mv)
-        else:
-            arr = (ctypes.c_char * n).from_buffer(mv)
-        return ctypes.cast(arr, ctypes.c_void_p), arr
-    raise TypeError("expected a bytes-like object, got %r" % type(data))
+    """(pointer, keepalive) for any contiguous buffer (bytes, bytearray,
+    memoryview, numpy array, mmap), without copying it."""
+    import numpy as np
+    try:
+        mv = memoryview(data)
+    except TypeError:
+        raise TypeError("expected a bytes-like object, got %r" % type(data)) from None
+    if not mv.c_contiguous:
+        raise ValueError("buffer must be C-contiguous")
+    mv = mv.cast("B")
+    if mv.nbytes == 0:
+        return None, b""
+    arr = np.frombuffer(mv, dtype=np.uint8)
+    return ctypes.c_void_p(arr.ctypes.data), (arr, mv)
 
 
 class Context:

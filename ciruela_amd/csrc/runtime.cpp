@@ -6,6 +6,7 @@
 
 #include <errno.h>
 #include <string.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -282,6 +283,37 @@ static int for_each_device(cir_ctx* ctx, const std::function<int(cir::Device&, s
 // short count at EOF.
 using Reader = std::function<int64_t(uint8_t*, uint64_t)>;
 
+// Run piece(off, len) over [0, n) in 8 MiB pieces on up to 16 host threads
+// (a staging batch is 256 MiB: one copying thread moves ~10 GB/s, the
+// upload takes ~55 GB/s).  Returns 0 or the first negative piece result;
+// a piece must return len on success.
+static int64_t parallel_pieces(uint64_t n, const std::function<int64_t(uint64_t, uint64_t)>& piece) {
+  constexpr uint64_t kPiece = 8ull << 20;
+  const uint64_t np = (n + kPiece - 1) / kPiece;
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const unsigned nt = (unsigned)std::min<uint64_t>(np, std::min(16u, hw));
+  std::atomic<uint64_t> next{0};
+  std::atomic<int64_t> err{0};
+  auto work = [&] {
+    for (uint64_t p; (p = next.fetch_add(1)) < np && err.load() == 0;) {
+      const uint64_t off = p * kPiece, len = std::min(kPiece, n - off);
+      const int64_t r = piece(off, len);
+      if (r != (int64_t)len) {
+        int64_t z = 0;
+        err.compare_exchange_strong(z, r < 0 ? r : -(int64_t)EIO);
+      }
+    }
+  };
+  if (nt <= 1) {
+    work();
+  } else {
+    std::vector<std::thread> th;
+    for (unsigned i = 0; i < nt; ++i) th.emplace_back(work);
+    for (auto& t : th) t.join();
+  }
+  return err.load();
+}
+
 static int run_file(cir_ctx* ctx, const Reader& rd, uint64_t bs, uint64_t* size_out,
                     std::vector<uint8_t>& hashes, int ht) {
   Device& d = *ctx->devs[0];
@@ -534,7 +566,40 @@ int cir_hash_file_ht(cir_ctx* ctx, int hash_type, int fd, uint64_t block_size,
     return fail(CIR_EINVAL, "block_size must be in 1 .. 2^32-1");
   if (!valid_hash_type(hash_type)) return fail(CIR_EINVAL, "unknown hash type");
   std::vector<uint8_t> h;
-  Reader rd = [fd](uint8_t* dst, uint64_t n) -> int64_t {
+  // Regular files: the bytes known to exist (st_size at the start) are read
+  // with pread() by several threads per batch, then the read position moves
+  // past them; beyond that (growth, pipes, sockets) plain read() to EOF,
+  // as Hashes::hash_file's Read loop does.
+  struct stat st;
+  const off_t pos0 = ::lseek(fd, 0, SEEK_CUR);
+  uint64_t known = 0, done = 0;
+  if (pos0 >= 0 && ::fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && st.st_size > pos0)
+    known = (uint64_t)(st.st_size - pos0);
+  Reader rd = [fd, pos0, &known, &done](uint8_t* dst, uint64_t n) -> int64_t {
+    if (done < known) {
+      const uint64_t k = std::min(n, known - done);
+      const uint64_t base = (uint64_t)pos0 + done;
+      const int64_t e = parallel_pieces(k, [&](uint64_t off, uint64_t len) -> int64_t {
+        uint64_t got = 0;
+        while (got < len) {
+          const ssize_t r = ::pread(fd, dst + off + got, len - got, (off_t)(base + off + got));
+          if (r < 0 && errno == EINTR) continue;
+          if (r < 0) return -(int64_t)errno;
+          if (r == 0) break;  // truncated meanwhile
+          got += (uint64_t)r;
+        }
+        return (int64_t)got;
+      });
+      if (e < 0 && e != -(int64_t)EIO) return e;
+      if (e == 0) {
+        done += k;
+        if (::lseek(fd, (off_t)(base + k), SEEK_SET) < 0) return -(int64_t)errno;
+        return (int64_t)k;
+      }
+      // shrank while hashing: fall back to sequential reads from here
+      known = done;
+      if (::lseek(fd, (off_t)base, SEEK_SET) < 0) return -(int64_t)errno;
+    }
     for (;;) {
       ssize_t r = ::read(fd, dst, n);
       if (r < 0 && errno == EINTR) continue;
@@ -561,7 +626,11 @@ int cir_hash_memory_ht(cir_ctx* ctx, int hash_type, const uint8_t* data, uint64_
   uint64_t pos = 0, got_size = 0;
   Reader rd = [&](uint8_t* dst, uint64_t n) -> int64_t {
     const uint64_t k = std::min(n, size - pos);
-    memcpy(dst, data + pos, k);
+    const uint8_t* src = data + pos;
+    parallel_pieces(k, [&](uint64_t off, uint64_t len) -> int64_t {
+      memcpy(dst + off, src + off, len);
+      return (int64_t)len;
+    });
     pos += k;
     return (int64_t)k;
   };

@@ -95,6 +95,10 @@ for s in "$@"; do
           > gpurun_out/cfg3ab.json 2> gpurun_out/cfg3ab.err
         echo "$lib $(cat gpurun_out/cfg3ab.json)"
       done ;;
+    cfg2host)
+      step cfg2host 600 python bench.py --workload config2host --steps 3 --host-gib "${HOST_GIB:-32}" \
+        > gpurun_out/cfg2host.json 2> gpurun_out/cfg2host.err
+      cat gpurun_out/cfg2host.json ;;
     cfg1)
       step cfg1 300 python bench.py --workload config1 > gpurun_out/cfg1.json 2> gpurun_out/cfg1.err
       cat gpurun_out/cfg1.json ;;
