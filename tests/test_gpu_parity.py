@@ -522,3 +522,37 @@ def test_concurrent_callers_one_context(gpu, small_ctx, oracle):
         t.join(timeout=120)
     assert not any(t.is_alive() for t in jobs)
     assert errors == []
+
+
+def test_hash_file_parallel_reads_offset_and_pipe(ctx, oracle, tmp_path):
+    """Regular files are read with pread by several threads per staging batch
+    starting at the fd's current offset, which ends at EOF (the reference
+    reads the Read object to its end); pipes go through plain read()."""
+    import threading
+    bs = 32768
+    data = os.urandom((21 << 20) + 5)
+    p = tmp_path / "big.bin"
+    p.write_bytes(data)
+    with open(p, "rb") as f:
+        f.seek(1000)
+        size, hashes = ctx.hash_file(f.fileno(), bs)
+        assert os.lseek(f.fileno(), 0, os.SEEK_CUR) == len(data)
+    tail = data[1000:]
+    assert size == len(tail)
+    assert hashes == b"".join(oracle_digest(oracle, tail[i:i + bs]) for i in range(0, len(tail), bs))
+    rfd, wfd = os.pipe()
+    payload = data[:(5 << 20) + 77]
+
+    def writer():
+        with os.fdopen(wfd, "wb") as w:
+            w.write(payload)
+    t = threading.Thread(target=writer)
+    t.start()
+    try:
+        size, hashes = ctx.hash_file(rfd, bs)
+    finally:
+        t.join()
+        os.close(rfd)
+    assert size == len(payload)
+    assert hashes == b"".join(oracle_digest(oracle, payload[i:i + bs])
+                              for i in range(0, len(payload), bs))
