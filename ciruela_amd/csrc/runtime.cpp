@@ -208,6 +208,57 @@ static int check_device(int id) {
 
 // ---- host-memory batch: cir_hash_blocks --------------------------------
 
+// Run piece(off, len) over [0, n) in 8 MiB pieces on up to 16 host threads
+// (a staging batch is 256 MiB: one copying thread moves ~10 GB/s, the
+// upload takes ~55 GB/s).  Returns 0 or the first negative piece result;
+// a piece must return len on success.
+static int64_t parallel_pieces(uint64_t n, const std::function<int64_t(uint64_t, uint64_t)>& piece) {
+  constexpr uint64_t kPiece = 8ull << 20;
+  const uint64_t np = (n + kPiece - 1) / kPiece;
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const unsigned nt = (unsigned)std::min<uint64_t>(np, std::min(16u, hw));
+  std::atomic<uint64_t> next{0};
+  std::atomic<int64_t> err{0};
+  auto work = [&] {
+    for (uint64_t p; (p = next.fetch_add(1)) < np && err.load() == 0;) {
+      const uint64_t off = p * kPiece, len = std::min(kPiece, n - off);
+      const int64_t r = piece(off, len);
+      if (r != (int64_t)len) {
+        int64_t z = 0;
+        err.compare_exchange_strong(z, r < 0 ? r : -(int64_t)EIO);
+      }
+    }
+  };
+  if (nt <= 1) {
+    work();
+  } else {
+    std::vector<std::thread> th;
+    for (unsigned i = 0; i < nt; ++i) th.emplace_back(work);
+    for (auto& t : th) t.join();
+  }
+  return err.load();
+}
+
+// fn(i0, i1) over [0, n) items in groups, on up to 16 host threads when the
+// batch moves at least 16 MiB (bytes); one thread otherwise.
+static void parallel_items(size_t n, uint64_t bytes, const std::function<void(size_t, size_t)>& fn) {
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const unsigned nt = bytes < (16ull << 20) ? 1u : std::min(16u, hw);
+  if (nt <= 1 || n < 2) {
+    fn(0, n);
+    return;
+  }
+  const size_t grain = std::max<size_t>(1, n / (8 * nt));
+  std::atomic<size_t> next{0};
+  auto work = [&] {
+    for (size_t i0; (i0 = next.fetch_add(grain)) < n;) fn(i0, std::min(n, i0 + grain));
+  };
+  std::vector<std::thread> th;
+  for (unsigned i = 0; i < nt; ++i) th.emplace_back(work);
+  for (auto& t : th) t.join();
+}
+
+
 // Hash blocks [b0, b1) of a host arena on device d, packing them 16-byte
 // aligned into the two staging slots (pack slot k+1 while slot k hashes).
 static int run_blocks(cir_ctx* ctx, Device& d, const uint8_t* arena, const uint64_t* off,
@@ -244,9 +295,14 @@ static int run_blocks(cir_ctx* ctx, Device& d, const uint8_t* arena, const uint6
         pos = (pos + 15) & ~15ull;
         s.h_off[i] = pos;
         s.h_len[i] = len[next + i];
-        memcpy(s.h_data + pos, arena + off[next + i], len[next + i]);
         pos += len[next + i];
       }
+      // gather the blocks into the slot on several threads
+      const size_t base = next;
+      parallel_items(n, pos, [&](size_t i0, size_t i1) {
+        for (size_t i = i0; i < i1; ++i)
+          memcpy(s.h_data + s.h_off[i], arena + off[base + i], s.h_len[i]);
+      });
       rc = slot_submit(d, s, std::max<uint64_t>(pos, 1), n, ht);
       if (rc) return rc;
       pending_first[k] = next;
@@ -283,36 +339,6 @@ static int for_each_device(cir_ctx* ctx, const std::function<int(cir::Device&, s
 // short count at EOF.
 using Reader = std::function<int64_t(uint8_t*, uint64_t)>;
 
-// Run piece(off, len) over [0, n) in 8 MiB pieces on up to 16 host threads
-// (a staging batch is 256 MiB: one copying thread moves ~10 GB/s, the
-// upload takes ~55 GB/s).  Returns 0 or the first negative piece result;
-// a piece must return len on success.
-static int64_t parallel_pieces(uint64_t n, const std::function<int64_t(uint64_t, uint64_t)>& piece) {
-  constexpr uint64_t kPiece = 8ull << 20;
-  const uint64_t np = (n + kPiece - 1) / kPiece;
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const unsigned nt = (unsigned)std::min<uint64_t>(np, std::min(16u, hw));
-  std::atomic<uint64_t> next{0};
-  std::atomic<int64_t> err{0};
-  auto work = [&] {
-    for (uint64_t p; (p = next.fetch_add(1)) < np && err.load() == 0;) {
-      const uint64_t off = p * kPiece, len = std::min(kPiece, n - off);
-      const int64_t r = piece(off, len);
-      if (r != (int64_t)len) {
-        int64_t z = 0;
-        err.compare_exchange_strong(z, r < 0 ? r : -(int64_t)EIO);
-      }
-    }
-  };
-  if (nt <= 1) {
-    work();
-  } else {
-    std::vector<std::thread> th;
-    for (unsigned i = 0; i < nt; ++i) th.emplace_back(work);
-    for (auto& t : th) t.join();
-  }
-  return err.load();
-}
 
 static int run_file(cir_ctx* ctx, const Reader& rd, uint64_t bs, uint64_t* size_out,
                     std::vector<uint8_t>& hashes, int ht) {
