@@ -241,6 +241,80 @@ __global__ __launch_bounds__(256, OCC) void k_comp_sm(uint8_t* out, uint32_t lin
   store_digest(out + b * 32u, h);
 }
 
+// Instruction-fetch probe: the same instruction mix with the 12 rounds rolled
+// into a loop (every round uses sigma_0, so the digests differ from BLAKE2b):
+// a ~1.3 KiB loop body instead of ~13 KiB of straight-line code.
+__device__ __forceinline__ void compress_rolled(uint64_t h[8], const uint64_t m[16], uint64_t t,
+                                                bool last) {
+  uint64_t v0 = h[0], v1 = h[1], v2 = h[2], v3 = h[3];
+  uint64_t v4 = h[4], v5 = h[5], v6 = h[6], v7 = h[7];
+  uint64_t v8 = CIR_IV0, v9 = CIR_IV1, v10 = CIR_IV2, v11 = CIR_IV3;
+  uint64_t v12 = CIR_IV4 ^ t, v13 = CIR_IV5;
+  uint64_t v14 = last ? ~CIR_IV6 : CIR_IV6, v15 = CIR_IV7;
+#pragma unroll 1
+  for (int r = 0; r < 12; ++r) {
+    CIR_ROUND_SM(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
+  }
+  sched_fence();
+  h[0] = xor3(h[0], v0, v8);
+  h[1] = xor3(h[1], v1, v9);
+  h[2] = xor3(h[2], v2, v10);
+  h[3] = xor3(h[3], v3, v11);
+  h[4] = xor3(h[4], v4, v12);
+  h[5] = xor3(h[5], v5, v13);
+  h[6] = xor3(h[6], v6, v14);
+  h[7] = xor3(h[7], v7, v15);
+}
+
+__global__ __launch_bounds__(256, 4) void k_comp_rolled(uint8_t* out, uint32_t lines) {
+  const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  uint64_t h[8], m[16];
+  init_state(h);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) m[k] = b * 0x9e3779b97f4a7c15ULL + k;
+  for (uint32_t i = 0; i < lines; ++i) {
+    m[0] ^= i;
+    compress_rolled(h, m, (uint64_t)(i + 1) * 128u, i + 1 == lines);
+  }
+  store_digest(out + b * 32u, h);
+}
+
+// same, unrolled (same wrong sigma): isolates the code-size effect
+__device__ __forceinline__ void compress_unrolled_s0(uint64_t h[8], const uint64_t m[16], uint64_t t,
+                                                     bool last) {
+  uint64_t v0 = h[0], v1 = h[1], v2 = h[2], v3 = h[3];
+  uint64_t v4 = h[4], v5 = h[5], v6 = h[6], v7 = h[7];
+  uint64_t v8 = CIR_IV0, v9 = CIR_IV1, v10 = CIR_IV2, v11 = CIR_IV3;
+  uint64_t v12 = CIR_IV4 ^ t, v13 = CIR_IV5;
+  uint64_t v14 = last ? ~CIR_IV6 : CIR_IV6, v15 = CIR_IV7;
+#pragma unroll
+  for (int r = 0; r < 12; ++r) {
+    CIR_ROUND_SM(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
+  }
+  sched_fence();
+  h[0] = xor3(h[0], v0, v8);
+  h[1] = xor3(h[1], v1, v9);
+  h[2] = xor3(h[2], v2, v10);
+  h[3] = xor3(h[3], v3, v11);
+  h[4] = xor3(h[4], v4, v12);
+  h[5] = xor3(h[5], v5, v13);
+  h[6] = xor3(h[6], v6, v14);
+  h[7] = xor3(h[7], v7, v15);
+}
+
+__global__ __launch_bounds__(256, 4) void k_comp_unrolled_s0(uint8_t* out, uint32_t lines) {
+  const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  uint64_t h[8], m[16];
+  init_state(h);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) m[k] = b * 0x9e3779b97f4a7c15ULL + k;
+  for (uint32_t i = 0; i < lines; ++i) {
+    m[0] ^= i;
+    compress_unrolled_s0(h, m, (uint64_t)(i + 1) * 128u, i + 1 == lines);
+  }
+  store_digest(out + b * 32u, h);
+}
+
 // MODE < 0: production compress()
 template <int MODE>
 __global__ __launch_bounds__(256, 4) void k_comp(uint8_t* out, uint32_t lines) {
@@ -317,6 +391,18 @@ int main() {
       printf("pass %d %-45s %8.3f ms  %7.1f GB/s-equivalent  %s\n", pass, k.name, t,
              (double)nlanes * 32768 / (t * 1e-3) / 1e9, ok ? "digests ok" : "DIGEST MISMATCH");
     }
+  }
+  {
+    struct {
+      const char* name;
+      CompKernel k;
+    } kf[] = {{"fetch probe: rounds unrolled, sigma_0 everywhere", k_comp_unrolled_s0},
+              {"fetch probe: rounds rolled (1-round loop body)", k_comp_rolled}};
+    for (int pass = 0; pass < 2; ++pass)
+      for (auto& k : kf) {
+        const float t = time_comp(k.k, dout, nlanes, 5);
+        printf("%-52s %8.3f ms  (digests are not BLAKE2b)\n", k.name, t);
+      }
   }
   for (auto& k : k2) {
     hipLaunchKernelGGL(k.k, dim3(nlanes / 512), dim3(256), 0, 0, dout, 256u);
