@@ -122,6 +122,9 @@ for s in "$@"; do
         --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 1 --steps 5 --warmup 1 --force-dist \
         --no-cpu-baseline > gpurun_out/dist1.json 2> gpurun_out/dist1.err
       cat gpurun_out/dist1.json ;;
+    asmg)
+      step asmg 300 ./build/asm_g_ubench > gpurun_out/asmg.log 2>&1
+      cat gpurun_out/asmg.log ;;
     dvfs)
       step dvfs 300 ./build/dvfs_probe > gpurun_out/dvfs.log 2>&1
       cat gpurun_out/dvfs.log ;;
