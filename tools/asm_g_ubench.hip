@@ -19,6 +19,10 @@ __global__ __launch_bounds__(256, OCC) void k_asm(uint32_t* out, int iters) {
     if constexpr (K == 0) asm volatile(ASM_HALF_GMAJOR ::: CLOBBERS);
     if constexpr (K == 1) asm volatile(ASM_HALF_RR ::: CLOBBERS);
     if constexpr (K == 2) asm volatile(ASM_HALF_STEP ::: CLOBBERS);
+    if constexpr (K == 3) asm volatile(ASM_HALF_STEP_SMSG ::: CLOBBERS, "s40", "s41", "s42", "s43");
+    if constexpr (K == 4) asm volatile(ASM_HALF_STEP_ALIGNXOR ::: CLOBBERS);
+    if constexpr (K == 5) asm volatile(ASM_HALF_STEP_ADDXOR ::: CLOBBERS);
+    if constexpr (K == 6) asm volatile(ASM_HALF_INDEP_MIX ::: CLOBBERS);
   }
   uint32_t v;
   asm volatile("v_mov_b32 %0, v10" : "=v"(v));
@@ -38,7 +42,11 @@ int main() {
             {"round-robin over 4 G      occ 5", k_asm<1, 5>},
             {"step-major (production)   occ 5", k_asm<2, 5>},
             {"G-major                   occ 8", k_asm<0, 8>},
-            {"step-major                occ 8", k_asm<2, 8>}};
+            {"step-major                occ 8", k_asm<2, 8>},
+            {"step-major, messages in SGPRs (probe)    occ 5", k_asm<3, 5>},
+            {"step-major, alignbit -> v_xor (probe)    occ 5", k_asm<4, 5>},
+            {"step-major, 64-bit add -> v_xor (probe)  occ 5", k_asm<5, 5>},
+            {"same class mix, no dependencies (probe)  occ 5", k_asm<6, 5>}};
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);

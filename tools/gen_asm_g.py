@@ -64,3 +64,49 @@ for kind in ("gmajor", "rr", "step"):
     body = "\\n".join(ins)
     print(f'#define ASM_HALF_{kind.upper()} "{body}\\n"')
 print(f"#define ASM_TOP_REG {top}")
+
+
+def variant(kind, sgpr_msg=False, align_as_xor=False, add_as_xor=False):
+    ins, top = order(kind)
+    out = []
+    for s in ins:
+        if sgpr_msg:
+            s = s.replace("v[58:59]", "s[40:41]").replace("v[60:61]", "s[42:43]")
+        if align_as_xor and s.startswith("v_alignbit_b32"):
+            parts = s.split(", ")
+            s = "v_xor_b32 " + parts[0].split()[1] + ", " + parts[1] + ", " + parts[2]
+        out.append(s)
+    return "\\n".join(out)
+
+def variant_addxor():
+    ins, top = order("step")
+    out = []
+    for s in ins:
+        if s.startswith("v_lshl_add_u64"):
+            # v_lshl_add_u64 v[a:a+1], v[a:a+1], 0, v[b:b+1] -> v_xor_b32 va, va, vb
+            parts = s.replace("v_lshl_add_u64 ", "").split(", ")
+            d = int(parts[0][2:].split(":")[0]); b = int(parts[3][2:].split(":")[0])
+            s = "v_xor_b32 v%d, v%d, v%d" % (d, d, b)
+        out.append(s)
+    return "\\n".join(out)
+
+def independent_mix():
+    # same class mix as one half-round (24 lshl_add, 24 alignbit, 32 xor) in
+    # step order, but no instruction depends on the previous 16
+    out = []
+    pattern = (["A"] * 8 + ["X"] * 8 + ["A"] * 4 + ["X"] * 8 + ["L"] * 8 + ["A"] * 8 + ["X"] * 8 +
+               ["L"] * 8 + ["A"] * 4 + ["X"] * 8 + ["L"] * 8)
+    ia = il = ix = 0
+    for c in pattern:
+        if c == "A":
+            r = 10 + 2 * (ia % 8); out.append("v_lshl_add_u64 v[%d:%d], v[%d:%d], 0, v[58:59]" % (r, r + 1, r, r + 1)); ia += 1
+        elif c == "L":
+            r = 26 + (il % 16); out.append("v_alignbit_b32 v%d, v%d, v59, 7" % (r, r)); il += 1
+        else:
+            r = 42 + (ix % 16); out.append("v_xor_b32 v%d, v%d, v60" % (r, r)); ix += 1
+    return "\\n".join(out)
+
+print('#define ASM_HALF_STEP_ADDXOR "%s\\n"' % variant_addxor())
+print('#define ASM_HALF_INDEP_MIX "%s\\n"' % independent_mix())
+print('#define ASM_HALF_STEP_SMSG "%s\\n"' % variant("step", sgpr_msg=True))
+print('#define ASM_HALF_STEP_ALIGNXOR "%s\\n"' % variant("step", align_as_xor=True))
