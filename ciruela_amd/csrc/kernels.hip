@@ -190,6 +190,22 @@ __device__ __forceinline__ void quad_run(uint64_t& h0, uint64_t& h1, uint64_t t0
   }
 }
 
+// The chain of quad q of this wave (block b at p, L bytes; have = false for a
+// quad past the end) is hashed into out + 32 b.
+template <bool kPrefetchAll>
+__device__ __forceinline__ void quad_chain(bool have, uint64_t b, const uint8_t* p, uint32_t L,
+                                           uint8_t* __restrict__ out, uint8_t* lds,
+                                           uint32_t wave_lds) {
+  const uint32_t lane = threadIdx.x & 63u, i = lane & 3u, q = lane >> 2;
+  const uint32_t line = wave_lds + q * 128u;  // this quad's line in LDS
+  uint32_t addr[48];
+  quad_addr(addr, line, i);
+  uint64_t h0, h1;
+  quad_init(i, h0, h1);
+  quad_run<kPrefetchAll>(h0, h1, 0, p, have ? L : 0u, have, true, lds, addr, line, i);
+  if (have) *reinterpret_cast<uint64_t*>(out + b * 32u + 8u * i) = h0;
+}
+
 template <bool kPrefetchAll>
 __device__ __forceinline__ void quad_chains(const uint8_t* __restrict__ arena,
                                             const uint64_t* __restrict__ off,
@@ -197,8 +213,7 @@ __device__ __forceinline__ void quad_chains(const uint8_t* __restrict__ arena,
                                             const uint32_t* __restrict__ perm, uint32_t first,
                                             uint32_t nlong, uint8_t* __restrict__ out,
                                             uint8_t* lds, uint32_t wave_lds) {
-  const uint32_t lane = threadIdx.x & 63u, i = lane & 3u, q = lane >> 2;
-  const uint32_t c = first + q;
+  const uint32_t c = first + ((threadIdx.x & 63u) >> 2);
   const bool have = c < nlong;
   uint32_t b = 0, L = 0;
   uint64_t o = 0;
@@ -207,14 +222,25 @@ __device__ __forceinline__ void quad_chains(const uint8_t* __restrict__ arena,
     o = off[b];
     L = len[b];
   }
-  const uint8_t* p = arena + o;
-  const uint32_t line = wave_lds + q * 128u;  // this quad's line in LDS
-  uint32_t addr[48];
-  quad_addr(addr, line, i);
-  uint64_t h0, h1;
-  quad_init(i, h0, h1);
-  quad_run<kPrefetchAll>(h0, h1, 0, p, have ? L : 0u, have, true, lds, addr, line, i);
-  if (have) *reinterpret_cast<uint64_t*>(out + (uint64_t)b * 32u + 8u * i) = h0;
+  quad_chain<kPrefetchAll>(have, b, arena + o, L, out, lds, wave_lds);
+}
+
+// Hashes::hash_file split of one device-resident file with fewer than
+// kQuadSmallBatch blocks: every block in quad mode (16 per wave).
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_quad_chunks(
+    const uint8_t* __restrict__ data, uint64_t nbytes, uint64_t bs, uint64_t nblk,
+    uint8_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kWaves * kQuadWaveLds];
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t first = ((uint64_t)blockIdx.x * kWaves + wave) * 16u;
+  if (first >= nblk) return;
+  __builtin_amdgcn_s_setprio(3);
+  const uint64_t b = first + ((threadIdx.x & 63u) >> 2);
+  const bool have = b < nblk;
+  const uint64_t o = have ? b * bs : 0;
+  const uint64_t rest = nbytes - o;
+  quad_chain<true>(have, b, data + o, have ? (uint32_t)(rest < bs ? rest : bs) : 0u, out, lds,
+                   wave * kQuadWaveLds);
 }
 
 // Quad part of an ordered batch: chains [0, nl), nl = min(*n_long, 64 nq_wg).
@@ -399,6 +425,11 @@ hipError_t launch_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint
   if (nbytes == 0) return hipSuccess;
   if (bs == 0) return hipErrorInvalidValue;
   const uint64_t nblk = (nbytes + bs - 1) / bs;
+  if (nblk < kQuadSmallBatch && bs >= 128ull * kQuadSmallMinLines && bs <= 0xffffffffull) {
+    hipLaunchKernelGGL(k_quad_chunks, dim3((unsigned)((nblk + 63) / 64)), dim3(kThreads), 0, s,
+                       data, nbytes, bs, nblk, out);
+    return hipGetLastError();
+  }
   const bool uni_ok = bs % 128u == 0 && (reinterpret_cast<uintptr_t>(data) & 15u) == 0 &&
                       bs / 128u <= 0xffffffffull && bs <= 0xffffffffull / 8u;
   const uint64_t nuni = uni_ok ? (nbytes / bs) / kThreads * kThreads : 0;
@@ -431,7 +462,7 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
                         const uint32_t* perm, const uint32_t* n_long, uint64_t n, uint8_t* out,
                         hipStream_t s, hipStream_t aux, hipEvent_t fork, hipEvent_t join) {
   if (n == 0) return hipSuccess;
-  const uint64_t nq = std::min<uint64_t>((n + 63) / 64, (uint64_t)kQuadMaxWg);
+  const uint64_t nq = std::min<uint64_t>((n + 63) / 64, quad_max_wg(n));
   const uint64_t lane_grid = grid_for(n, kThreads);
   if (lane_grid > 0x7fffffffull) return hipErrorInvalidValue;
   hipError_t e = hipEventRecord(fork, s);

@@ -20,6 +20,24 @@ enum class Loader : int { kGlds = 0, kDirect = 1 };
 constexpr uint32_t kQuadMinLines = CIR_QUAD_MIN_LINES;
 constexpr int kQuadMaxWg = 256;  // at most 256 x 64 = 16384 chains in quad mode
 
+// Small batches: lane mode is latency-bound below about one wave per SIMD
+// (64 x 1024 = 65536 chains; lane mode measured 2232 GiB/s at 8 M x 4 KiB
+// but 1024 GiB/s at 32 K x 1 MiB and 258 at 8 K x 4 MiB).  Batches of at
+// most 49152 chains run every chain of at least kQuadSmallMinLines lines in
+// quad mode (4 x the waves, ~1/3 the latency per compression): 1537-1638
+// GiB/s at 32 K x 1 MiB, 737 at 8 K x 4 MiB.  The two modes cross at ~49152
+// chains (within 4 % there at 32 KiB, 256 KiB and 1 MiB); at 65535 lane
+// mode is ahead (1548 vs 1335 GiB/s at 32 KiB, 1928 vs 1567 at 256 KiB;
+// profiles/r01/shapes.log).
+constexpr uint64_t kQuadSmallBatch = 49153;
+constexpr uint32_t kQuadSmallMinLines = 8;
+inline uint32_t quad_min_lines(uint64_t n) {
+  return n < kQuadSmallBatch ? kQuadSmallMinLines : kQuadMinLines;
+}
+inline uint64_t quad_max_wg(uint64_t n) {
+  return n < kQuadSmallBatch ? (n + 63) / 64 : (uint64_t)kQuadMaxWg;
+}
+
 // nblk equal blocks of bs bytes at data (bs % 128 == 0, data 16-byte aligned,
 // nblk % 256 == 0).  out: nblk x 32 bytes.
 hipError_t launch_uniform(Loader loader, const uint8_t* data, uint64_t bs, uint64_t nblk,
@@ -41,7 +59,7 @@ hipError_t launch_general_desc(const uint8_t* arena, const uint64_t* off, const 
                                const uint32_t* perm, uint64_t n, uint8_t* out, hipStream_t s);
 
 // Descriptor batch in the order perm (longest chain first); the first
-// min(*n_long, 64 * kQuadMaxWg) chains (device count) run in quad mode on s,
+// min(*n_long, 64 * quad_max_wg(n)) chains (device count) run in quad mode on s,
 // the rest one lane per chain on `aux` (forked from s with `fork`, joined
 // back into s with `join`).
 hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
@@ -51,7 +69,7 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
 // Longest-chain-first order of a descriptor batch (order.hip): *perm points
 // into `scratch` (order_scratch_bytes(n) bytes, device memory).
 size_t order_scratch_bytes(uint64_t n);
-// *n_long = number of chains with >= kQuadMinLines lines (device memory).
+// *n_long = number of chains with >= quad_min_lines(n) lines (device memory).
 hipError_t launch_order_desc(const uint32_t* len, uint64_t n, void* scratch, size_t bytes,
                              uint32_t** perm, uint32_t** n_long, hipStream_t s);
 

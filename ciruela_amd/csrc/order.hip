@@ -12,7 +12,7 @@
 namespace cir {
 namespace dev {
 
-__global__ void k_chain_keys(const uint32_t* __restrict__ len, uint64_t n,
+__global__ void k_chain_keys(const uint32_t* __restrict__ len, uint64_t n, uint32_t min_lines,
                              uint32_t* __restrict__ key, uint32_t* __restrict__ idx,
                              uint32_t* __restrict__ n_long) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -21,7 +21,7 @@ __global__ void k_chain_keys(const uint32_t* __restrict__ len, uint64_t n,
   const uint32_t k = l == 0 ? 1u : (l >> 7) + ((l & 127u) != 0);  // compressions, <= 2^25
   key[i] = k;
   idx[i] = (uint32_t)i;
-  if (k >= kQuadMinLines) atomicAdd(n_long, 1u);
+  if (k >= min_lines) atomicAdd(n_long, 1u);
 }
 
 size_t order_scratch_bytes(uint64_t n) {
@@ -48,7 +48,7 @@ hipError_t launch_order_desc(const uint32_t* len, uint64_t n, void* scratch, siz
   void* temp = p + 4 * arr;
   size_t temp_bytes = bytes - 4 * arr;
   hipLaunchKernelGGL(k_chain_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, len, n,
-                     key_in, idx_in, count);
+                     quad_min_lines(n), key_in, idx_in, count);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   e = hipcub::DeviceRadixSort::SortPairsDescending(temp, temp_bytes, key_in, key_out, idx_in,

@@ -107,6 +107,12 @@ def test_hash_bytes(gpu, oracle):
     (1000, 50000),                   # bs not a multiple of 128: unaligned blocks
     (4097, 300001),
     (65536, 512 * 65536),
+    # >= kQuadSmallBatch blocks: the lane-mode launch (LDS-DMA body + fused
+    # ragged rest, or the general loader when bs % 128 != 0)
+    (4096, 70000 * 4096 + 1234),
+    (1000, 70000 * 1000 + 7),
+    (128, 65536 * 128),
+    (32768, 49152 * 32768 + 99),   # one block past the quad-mode batch limit
 ])
 def test_chunks_dev_vs_oracle(gpu, ctx, oracle, bs, nbytes):
     import torch

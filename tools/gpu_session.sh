@@ -99,6 +99,13 @@ for s in "$@"; do
       step cfg2host 600 python bench.py --workload config2host --steps 3 --host-gib "${HOST_GIB:-32}" \
         > gpurun_out/cfg2host.json 2> gpurun_out/cfg2host.err
       cat gpurun_out/cfg2host.json ;;
+    shapes)
+      for sh in ${SHAPES:-4096_8388608 131072_262144 1048576_32768 4194304_8192 32768_65535 32768_65536 32768_16384 262144_65535 262144_65536}; do
+        set -- ${sh/_/ }
+        step "bs$1" 300 python bench.py --block-size $1 --blocks $2 --steps 5 --warmup 1 --no-cpu-baseline \
+          > gpurun_out/shape.json 2> gpurun_out/shape.err
+        echo "bs=$1 nblk=$2 $(grep -o '"value": [0-9.]*' gpurun_out/shape.json) $(grep -o '"kernel_ms_avg": [0-9.]*' gpurun_out/shape.json)"
+      done ;;
     cfg1)
       step cfg1 300 python bench.py --workload config1 > gpurun_out/cfg1.json 2> gpurun_out/cfg1.err
       cat gpurun_out/cfg1.json ;;
