@@ -340,9 +340,8 @@ static int for_each_device(cir_ctx* ctx, const std::function<int(cir::Device&, s
 using Reader = std::function<int64_t(uint8_t*, uint64_t)>;
 
 
-static int run_file(cir_ctx* ctx, const Reader& rd, uint64_t bs, uint64_t* size_out,
-                    std::vector<uint8_t>& hashes, int ht) {
-  Device& d = *ctx->devs[0];
+static int run_file_dev(cir_ctx* ctx, Device& d, const Reader& rd, uint64_t bs,
+                        uint64_t* size_out, std::vector<uint8_t>& hashes, int ht) {
   std::lock_guard<std::mutex> lk(d.mu);
   CIR_HIP(hipSetDevice(d.id));
   uint64_t chunk = ctx->staging / bs * bs;
@@ -394,6 +393,57 @@ static int run_file(cir_ctx* ctx, const Reader& rd, uint64_t bs, uint64_t* size_
     k ^= 1;
   }
   *size_out = total;
+  return CIR_OK;
+}
+
+static int run_file(cir_ctx* ctx, const Reader& rd, uint64_t bs, uint64_t* size_out,
+                    std::vector<uint8_t>& hashes, int ht) {
+  return run_file_dev(ctx, *ctx->devs[0], rd, bs, size_out, hashes, ht);
+}
+
+// read(dst, n, off): exactly n bytes at offset off (known to exist), or < 0.
+using PosReader = std::function<int64_t(uint8_t*, uint64_t, uint64_t)>;
+
+// A source of known size on a context with several devices: the blocks are
+// split into one contiguous range per device (equal counts), each hashed by
+// its own thread through that device's staging slots.
+static int run_split(cir_ctx* ctx, const PosReader& prd, uint64_t total, uint64_t bs,
+                     std::vector<uint8_t>& hashes, int ht) {
+  const uint64_t nblk = (total + bs - 1) / bs;
+  const size_t nd = std::min<size_t>(ctx->devs.size(), nblk);
+  hashes.assign(32 * nblk, 0);
+  std::vector<uint64_t> lo(nd), hi(nd);
+  for (size_t i = 0; i < nd; ++i) {
+    lo[i] = nblk * i / nd;
+    hi[i] = nblk * (i + 1) / nd;
+  }
+  std::vector<int> rc(nd, 0);
+  std::vector<std::string> err(nd);
+  std::vector<std::thread> th;
+  for (size_t i = 0; i < nd; ++i)
+    th.emplace_back([&, i] {
+      const uint64_t beg = lo[i] * bs, end = std::min(hi[i] * bs, total);
+      uint64_t pos = beg;
+      Reader rd = [&](uint8_t* dst, uint64_t n) -> int64_t {
+        const uint64_t k = std::min(n, end - pos);
+        if (k == 0) return 0;
+        const int64_t r = prd(dst, k, pos);
+        if (r < 0) return r;
+        pos += k;
+        return (int64_t)k;
+      };
+      std::vector<uint8_t> h;
+      uint64_t got = 0;
+      rc[i] = run_file_dev(ctx, *ctx->devs[i], rd, bs, &got, h, ht);
+      if (!rc[i] && h.size() != 32 * (hi[i] - lo[i])) rc[i] = fail(CIR_EIO, "short range");
+      if (rc[i])
+        err[i] = t_last_error;
+      else
+        memcpy(hashes.data() + 32 * lo[i], h.data(), h.size());
+    });
+  for (auto& t : th) t.join();
+  for (size_t i = 0; i < nd; ++i)
+    if (rc[i]) return fail(rc[i], err[i]);
   return CIR_OK;
 }
 
@@ -457,6 +507,22 @@ int cir_init(cir_ctx** out, uint32_t device_mask, uint64_t staging_bytes) {
     ctx->devs.push_back(std::move(d));
   }
   if (ctx->devs.empty()) return fail(CIR_ENODEV, "device_mask selects no visible device");
+  // CIR_DEBUG_SPLIT=k (tests): every selected GPU appears k times, as k
+  // independent device states (own streams, staging slots, scratch), so the
+  // multi-device splits of the host paths run on a one-GPU box.
+  if (const char* v = std::getenv("CIR_DEBUG_SPLIT")) {
+    const int k = std::atoi(v);
+    const size_t n0 = ctx->devs.size();
+    for (int r = 1; r < k && r < 8; ++r)
+      for (size_t i = 0; i < n0; ++i) {
+        auto d = std::make_unique<Device>();
+        d->id = ctx->devs[i]->id;
+        CIR_HIP(hipSetDevice(d->id));
+        CIR_HIP(hipStreamCreateWithFlags(&d->compute, hipStreamNonBlocking));
+        CIR_HIP(hipStreamCreateWithFlags(&d->copy, hipStreamNonBlocking));
+        ctx->devs.push_back(std::move(d));
+      }
+  }
   *out = ctx.release();
   return CIR_OK;
 }
@@ -601,6 +667,36 @@ int cir_hash_file_ht(cir_ctx* ctx, int hash_type, int fd, uint64_t block_size,
   uint64_t known = 0, done = 0;
   if (pos0 >= 0 && ::fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && st.st_size > pos0)
     known = (uint64_t)(st.st_size - pos0);
+  if (known > 0 && ctx->devs.size() > 1 && known > block_size) {
+    // several devices: split the known bytes, then make sure nothing follows
+    // (a file growing meanwhile is re-hashed on one device, to its end)
+    PosReader prd = [fd, pos0](uint8_t* dst, uint64_t n, uint64_t off) -> int64_t {
+      const int64_t e = parallel_pieces(n, [&](uint64_t o, uint64_t len) -> int64_t {
+        uint64_t got = 0;
+        while (got < len) {
+          const ssize_t r = ::pread(fd, dst + o + got, len - got, pos0 + (off_t)(off + o + got));
+          if (r < 0 && errno == EINTR) continue;
+          if (r <= 0) return r < 0 ? -(int64_t)errno : (int64_t)got;
+          got += (uint64_t)r;
+        }
+        return (int64_t)got;
+      });
+      return e < 0 ? e : (int64_t)n;
+    };
+    int rc = run_split(ctx, prd, known, block_size, h, hash_type);
+    if (rc) return rc;
+    uint8_t probe;
+    ssize_t more;
+    do more = ::pread(fd, &probe, 1, pos0 + (off_t)known);
+    while (more < 0 && errno == EINTR);
+    if (more == 0) {
+      if (::lseek(fd, pos0 + (off_t)known, SEEK_SET) < 0)
+        return fail(CIR_EIO, std::string("lseek: ") + strerror(errno));
+      *size_out = known;
+      return export_hashes(h, hashes_out, nhash_out);
+    }
+    known = 0;  // changed while hashed: fall through to the one-device read
+  }
   Reader rd = [fd, pos0, &known, &done](uint8_t* dst, uint64_t n) -> int64_t {
     if (done < known) {
       const uint64_t k = std::min(n, known - done);
@@ -649,6 +745,19 @@ int cir_hash_memory_ht(cir_ctx* ctx, int hash_type, const uint8_t* data, uint64_
   if (block_size == 0 || block_size > 0xffffffffull)
     return fail(CIR_EINVAL, "block_size must be in 1 .. 2^32-1");
   if (!valid_hash_type(hash_type)) return fail(CIR_EINVAL, "unknown hash type");
+  if (ctx->devs.size() > 1 && size > block_size) {
+    PosReader prd = [data](uint8_t* dst, uint64_t n, uint64_t off) -> int64_t {
+      parallel_pieces(n, [&](uint64_t o, uint64_t len) -> int64_t {
+        memcpy(dst + o, data + off + o, len);
+        return (int64_t)len;
+      });
+      return (int64_t)n;
+    };
+    std::vector<uint8_t> h;
+    int rc = run_split(ctx, prd, size, block_size, h, hash_type);
+    if (rc) return rc;
+    return export_hashes(h, hashes_out, nhash_out);
+  }
   uint64_t pos = 0, got_size = 0;
   Reader rd = [&](uint8_t* dst, uint64_t n) -> int64_t {
     const uint64_t k = std::min(n, size - pos);

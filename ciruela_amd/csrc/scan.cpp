@@ -175,22 +175,23 @@ static int run_reads(const std::vector<ReadJob>& jobs, const std::vector<ScanFil
 // while the previous batch uploads and hashes.
 using Progress = std::function<int(uint64_t done_blk)>;
 
-static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, unsigned threads,
-                      int ht, std::vector<uint8_t>& digests, const Progress& progress) {
-  uint64_t nblk_total = 0;
-  for (ScanFile& f : files) {
-    f.first_blk = nblk_total;
-    nblk_total += (f.size + bs - 1) / bs;
-  }
-  digests.assign(32 * nblk_total, 0);
-  if (nblk_total == 0) return CIR_OK;
-  Device& d = *ctx->devs[0];
+// Blocks [b0, b1) of the global block order on device d (files stay in
+// order; a range may start or end inside a file).  done(n) is called after
+// each batch with the number of blocks of the range finished so far (a
+// prefix of the range: the slots retire in submission order).
+static int hash_range(cir_ctx* ctx, Device& d, const std::vector<ScanFile>& files, uint64_t bs,
+                      unsigned threads, int ht, std::vector<uint8_t>& digests, uint64_t b0,
+                      uint64_t b1, const std::function<int(uint64_t)>& done) {
   std::lock_guard<std::mutex> lk(d.mu);
   CIR_HIP(hipSetDevice(d.id));
   const uint64_t cap = std::max<uint64_t>(ctx->staging, bs + 16);
   const uint64_t cap_blk = std::max<uint64_t>(cap / 512, 4096);
-  size_t fi = 0;       // current file
-  uint64_t fblk = 0;   // next block within it
+  // first file with a block >= b0
+  size_t fi = std::upper_bound(files.begin(), files.end(), b0,
+                               [](uint64_t b, const ScanFile& f) { return b < f.first_blk; }) -
+              files.begin();
+  fi = fi ? fi - 1 : 0;
+  uint64_t fblk = b0 > files[fi].first_blk ? b0 - files[fi].first_blk : 0;  // next block within it
   constexpr int kS = Device::kSlots;
   uint64_t pending_first[kS] = {}, pending_n[kS] = {};
   int k = 0;
@@ -204,7 +205,7 @@ static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, u
       ++fi;
       fblk = 0;
     }
-    return fi < files.size();
+    return fi < files.size() && files[fi].first_blk + fblk < b1;
   };
   while (more() || busy()) {
     Slot& s = d.slot[k];
@@ -217,11 +218,11 @@ static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, u
         (void)hipEventElapsedTime(&copy_ms, s.t_copy0, s.t_copy1);
         (void)hipEventElapsedTime(&gap_ms, s.t_copy1, s.t_hash0);
         (void)hipEventElapsedTime(&hash_ms, s.t_hash0, s.done);
-        fprintf(stderr, "cir_scan slot %d: h2d %.2f ms, h2d->hash %.2f ms, hash+d2h %.2f ms\n", k,
-                copy_ms, gap_ms, hash_ms);
+        fprintf(stderr, "cir_scan dev %d slot %d: h2d %.2f ms, h2d->hash %.2f ms, hash+d2h %.2f ms\n",
+                d.id, k, copy_ms, gap_ms, hash_ms);
       }
       memcpy(digests.data() + 32 * pending_first[k], s.h_out, 32 * pending_n[k]);
-      rc = progress(pending_first[k] + pending_n[k]);
+      rc = done(pending_first[k] + pending_n[k] - b0);
       if (rc) return rc;
     }
     const double t_wait1 = trace_on() ? now_ms() : 0;
@@ -232,8 +233,9 @@ static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, u
       uint64_t pos = 0, n = 0;
       const uint64_t first = files[fi].first_blk + fblk;
       while (more() && n < cap_blk) {
-        ScanFile& f = files[fi];
-        const uint64_t left_blk = (f.size + bs - 1) / bs - fblk;
+        const ScanFile& f = files[fi];
+        const uint64_t left_blk = std::min<uint64_t>((f.size + bs - 1) / bs - fblk,
+                                                     b1 - (f.first_blk + fblk));
         pos = (pos + 15) & ~15ull;
         if (pos + std::min<uint64_t>(bs, f.size - fblk * bs) > cap) break;
         // as many whole blocks of this file as fit
@@ -260,14 +262,74 @@ static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, u
       rc = slot_submit(d, s, std::max<uint64_t>(pos, 16), n, ht);
       if (rc) return rc;
       if (trace_on())
-        fprintf(stderr, "cir_scan batch: %.1f MiB, %zu jobs, wait %.2f ms, read %.2f ms (%.1f GB/s)\n",
-                pos / 1048576.0, jobs.size(), t_wait1 - t_wait0, t_read1 - t_read0,
+        fprintf(stderr, "cir_scan dev %d batch: %.1f MiB, %zu jobs, wait %.2f ms, read %.2f ms (%.1f GB/s)\n",
+                d.id, pos / 1048576.0, jobs.size(), t_wait1 - t_wait0, t_read1 - t_read0,
                 pos / 1e6 / std::max(t_read1 - t_read0, 1e-3));
       pending_first[k] = first;
       pending_n[k] = n;
     }
     k = (k + 1) % kS;
   }
+  return CIR_OK;
+}
+
+// Hash every block of every file; digests[32*g] for global block g.
+// Batches are packed into the staging slots of a device (file segments
+// 16-byte aligned, one descriptor per block) by `threads` reader threads
+// while the previous batches upload and hash.  With several devices in the
+// context the global block order is split into one contiguous range per
+// device (equal block counts), each driven by its own thread
+// with threads / ndev readers; progress(n) then reports the prefix of the
+// global order that is complete, called under a lock on device 0's
+// current-device setting (the emitter feeds device 0's footer chain).
+static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, unsigned threads,
+                      int ht, std::vector<uint8_t>& digests, const Progress& progress) {
+  uint64_t nblk_total = 0;
+  for (ScanFile& f : files) {
+    f.first_blk = nblk_total;
+    nblk_total += (f.size + bs - 1) / bs;
+  }
+  digests.assign(32 * nblk_total, 0);
+  if (nblk_total == 0) return CIR_OK;
+  const size_t nd = std::min<size_t>(ctx->devs.size(), nblk_total);
+  if (nd <= 1)
+    return hash_range(ctx, *ctx->devs[0], files, bs, threads, ht, digests, 0, nblk_total, progress);
+  std::vector<uint64_t> lo(nd), hi(nd), got(nd, 0);
+  for (size_t i = 0; i < nd; ++i) {
+    lo[i] = nblk_total * i / nd;
+    hi[i] = nblk_total * (i + 1) / nd;
+  }
+  std::mutex mu;
+  const int dev0 = ctx->devs[0]->id;
+  auto done = [&](size_t i, uint64_t n) -> int {
+    std::lock_guard<std::mutex> lk(mu);
+    got[i] = n;
+    uint64_t prefix = 0;
+    for (size_t j = 0; j < nd; ++j) {
+      prefix = lo[j] + got[j];
+      if (got[j] < hi[j] - lo[j]) break;
+    }
+    int cur = 0;
+    CIR_HIP(hipGetDevice(&cur));
+    CIR_HIP(hipSetDevice(dev0));
+    const int rc = progress(prefix);
+    CIR_HIP(hipSetDevice(cur));
+    return rc;
+  };
+  const unsigned per = std::max(1u, threads / (unsigned)nd);
+  std::vector<int> rc(nd, 0);
+  std::vector<std::string> err(nd);
+  std::vector<std::thread> th;
+  for (size_t i = 0; i < nd; ++i)
+    th.emplace_back([&, i] {
+      rc[i] = hash_range(ctx, *ctx->devs[i], files, bs, per, ht, digests, lo[i], hi[i],
+                         [&, i](uint64_t n) { return done(i, n); });
+      if (rc[i]) err[i] = cir_last_error();
+    });
+  for (auto& t : th) t.join();
+  for (size_t i = 0; i < nd; ++i)
+    if (rc[i]) return fail(rc[i], err[i]);
+  CIR_HIP(hipSetDevice(dev0));
   return CIR_OK;
 }
 

@@ -562,3 +562,43 @@ def test_hash_file_parallel_reads_offset_and_pipe(ctx, oracle, tmp_path):
     assert size == len(payload)
     assert hashes == b"".join(oracle_digest(oracle, payload[i:i + bs])
                               for i in range(0, len(payload), bs))
+
+
+def test_multi_device_split_paths(gpu, oracle, tmp_path):
+    """The host paths' multi-device splits (one contiguous
+    block range per device, one thread each), run on one GPU through
+    CIR_DEBUG_SPLIT=3 (the GPU appears as three independent device states):
+    hash_memory, hash_file from an offset, hash_blocks, and a directory scan
+    whose footer chain is fed from the device threads."""
+    os.environ["CIR_DEBUG_SPLIT"] = "3"
+    try:
+        ctx = gpu.Context(device_mask=1, staging_bytes=1 << 20)
+    finally:
+        del os.environ["CIR_DEBUG_SPLIT"]
+    assert len(ctx.devices()) == 3
+    rng = random.Random(33)
+    bs = 32768
+    data = rng.randbytes((10 << 20) + 5)
+    want = b"".join(oracle_digest(oracle, data[i:i + bs]) for i in range(0, len(data), bs))
+    assert ctx.hash_memory(data, bs) == want
+    p = tmp_path / "f.bin"
+    p.write_bytes(data)
+    with open(p, "rb") as f:
+        f.seek(100)
+        size, hashes = ctx.hash_file(f.fileno(), bs)
+        assert os.lseek(f.fileno(), 0, os.SEEK_CUR) == len(data)
+    assert size == len(data) - 100
+    assert hashes == b"".join(oracle_digest(oracle, data[100 + i:100 + i + bs])
+                              for i in range(0, len(data) - 100, bs))
+    lens = [rng.choice([0, 1, 4096, bs, rng.randrange(1, 200000)]) for _ in range(500)]
+    offs = [rng.randrange(0, len(data) - ln + 1) for ln in lens]
+    got = ctx.hash_blocks(data, offs, lens)
+    assert got == b"".join(oracle_digest(oracle, data[o:o + ln]) for o, ln in zip(offs, lens))
+    tree = tmp_path / "tree"
+    for k in range(12):
+        d = tree / ("d%d" % (k % 3))
+        d.mkdir(parents=True, exist_ok=True)
+        (d / ("f%02d" % k)).write_bytes(rng.randbytes(rng.choice([0, 1, 5000, 70000, 1 << 20])))
+    for block_size in (32768, 1024):
+        cfg = gpu.ScannerConfig.new().block_size(block_size).threads(4).add_dir(str(tree), "/")
+        assert gpu.v1.scan(cfg, context=ctx) == dirsig_oracle.scan(str(tree), block_size)
