@@ -53,7 +53,8 @@ def parse():
     p.add_argument("--block-size", type=int, default=32768)
     p.add_argument("--loader", choices=["glds", "direct", "api"], default="api",
                    help="api = cir_hash_chunks_dev (production path, LDS-DMA loader)")
-    p.add_argument("--workload", choices=["auto", "config3", "config5", "config1", "config2host"],
+    p.add_argument("--workload", choices=["auto", "config3", "config5", "config1", "config2host",
+                                          "config2sha"],
                    default="auto", help="auto = config2 at N=1, config4 at N>1")
     p.add_argument("--tree-gib", type=float, default=50.0, help="config5 tree size")
     p.add_argument("--host-gib", type=int, default=32, help="config2host buffer size")
@@ -239,6 +240,39 @@ def run_config2host(args, ca, ctx, dev, stream):
                     "k_chunks -> D2H digests, double-buffered"}
 
 
+def run_config2sha(args, ca, ctx, dev, stream):
+    """Config 2's blocks (1 M x 32 KiB, device-resident) hashed with
+    dir-signature's second hash type, SHA-512/256 (row f4), through the
+    descriptor entry point cir_hash_blocks_dev_ht."""
+    import torch
+    bs, nblk = args.block_size, args.blocks
+    data = torch.empty(nblk * bs, dtype=torch.uint8, device=dev)
+    fill_config2(ca, data, bs, stream)
+    d_off = torch.arange(nblk, dtype=torch.int64, device=dev) * bs
+    d_len = torch.full((nblk,), bs, dtype=torch.int32, device=dev)
+    out = torch.empty(nblk * 32, dtype=torch.uint8, device=dev)
+
+    def step():
+        ctx.hash_blocks_dev(data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), nblk,
+                            out.data_ptr(), stream, ca.HashType.sha512_256())
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    import hashlib
+    ok = all(out[32 * i:32 * i + 32].cpu().numpy().tobytes() ==
+             hashlib.new("sha512_256", data[i * bs:(i + 1) * bs].cpu().numpy().tobytes()).digest()
+             for i in (0, 20, nblk - 1))
+    return {"metric": "GiB/s SHA-512/256 block-hashed, config 2 shape (device-resident)",
+            "value": round(nblk * bs / dt / GIB, 3), "unit": "GiB/s",
+            "ms_per_step": round(dt * 1e3, 3), "steps": args.steps, "blocks": nblk,
+            "block_size": bs, "spot_check_vs_hashlib": ok}
+
+
 def make_tree(root, gib, file_mib=32, ndirs=40, seed=0x5EED0005):
     """Config 5 tree: files of file_mib MiB in ndirs directories."""
     import numpy as np
@@ -342,7 +376,8 @@ def main():
         rec = {"config3": lambda: run_config3(args, ca, ctx, dev, stream),
                "config5": lambda: run_config5(args, ca, ctx),
                "config1": lambda: run_config1(args, ca, ctx),
-               "config2host": lambda: run_config2host(args, ca, ctx, dev, stream)}[args.workload]()
+               "config2host": lambda: run_config2host(args, ca, ctx, dev, stream),
+               "config2sha": lambda: run_config2sha(args, ca, ctx, dev, stream)}[args.workload]()
         print(json.dumps(rec), flush=True)
         return 0
 
