@@ -561,6 +561,8 @@ int cir_hash_chunks_dev(cir_ctx* ctx, const void* d_data, uint64_t nbytes, uint6
   (void)ctx;
   if (block_size == 0) return fail(CIR_EINVAL, "block_size must be > 0");
   if (nbytes && (!d_data || !d_out)) return fail(CIR_EINVAL, "null device pointer");
+  if (reinterpret_cast<uintptr_t>(d_out) & 15u)
+    return fail(CIR_EINVAL, "d_out must be 16-byte aligned");
   CIR_HIP(dev::launch_chunks((const uint8_t*)d_data, nbytes, block_size, d_out,
                              (hipStream_t)stream));
   return CIR_OK;
@@ -572,6 +574,8 @@ int cir_hash_blocks_dev_ht(cir_ctx* ctx, int hash_type, const void* d_arena,
   if (!valid_hash_type(hash_type)) return fail(CIR_EINVAL, "unknown hash type");
   if (nblk && (!d_arena || !d_off || !d_len || !d_out))
     return fail(CIR_EINVAL, "null device pointer");
+  if (reinterpret_cast<uintptr_t>(d_out) & 15u)
+    return fail(CIR_EINVAL, "d_out must be 16-byte aligned");
   if (nblk > 0xffffffffull) return fail(CIR_EINVAL, "more than 2^32 descriptors");
   hipStream_t s = (hipStream_t)stream;
   // Context-less calls hash in descriptor order, one lane per chain; with a

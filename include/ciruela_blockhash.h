@@ -76,14 +76,15 @@ int cir_blake2b256(const uint8_t* p, size_t n, uint8_t out[CIR_DIGEST_BYTES]);
 
 /* Device-resident Hashes::hash_file: the bytes [d_data, d_data + nbytes) of
  * one file already in HBM, split into ceil(nbytes / block_size) blocks (the
- * last one short; none when nbytes == 0), digest i -> d_out + 32 i.  This is
- * the metric path (BASELINE.json configs 2 and 4). */
+ * last one short; none when nbytes == 0), digest i -> d_out + 32 i (d_out
+ * 16-byte aligned, as hipMalloc returns it).  This is the metric path
+ * (BASELINE.json configs 2 and 4). */
 int cir_hash_chunks_dev(cir_ctx* ctx, const void* d_data, uint64_t nbytes, uint64_t block_size,
                         uint8_t* d_out, void* stream);
 
 /* Device-resident batch of independent blocks: block b = d_arena[d_off[b] ..
- * d_off[b] + d_len[b]) -> d_out + 32 b.  Any order, any mix of lengths
- * (config 3); zero-length blocks hash as the empty input. */
+ * d_off[b] + d_len[b]) -> d_out + 32 b (d_out 16-byte aligned).  Any order,
+ * any mix of lengths (config 3); zero-length blocks hash as the empty input. */
 int cir_hash_blocks_dev(cir_ctx* ctx, const void* d_arena, const uint64_t* d_off,
                         const uint32_t* d_len, size_t nblk, uint8_t* d_out, void* stream);
 

@@ -96,13 +96,14 @@ def test_hash_bytes(gpu, oracle):
 
 
 @pytest.mark.parametrize("bs,nbytes", [
-    (32768, 256 * 32768),            # exactly one uniform workgroup
-    (32768, 512 * 32768 + 1000),     # uniform + short tail fused in one launch
-    (32768, 300 * 32768 + 5),        # uniform + 44 full general blocks + tail
-    (32768, 100 * 32768),            # < 256 blocks: general path only
+    # < kQuadSmallBatch blocks of >= 8 lines: quad mode (k_quad_chunks)
+    (32768, 256 * 32768),
+    (32768, 512 * 32768 + 1000),     # + a short tail
+    (32768, 300 * 32768 + 5),
+    (32768, 100 * 32768),
     (32768, 1), (32768, 127), (32768, 128), (32768, 129), (32768, 32768),
     (4096, 1000 * 4096),
-    (128, 1024 * 128 + 64),
+    (128, 1024 * 128 + 64),          # 1-line blocks: lane mode at any count
     (1 << 20, 3 * (1 << 20) + 7),
     (1000, 50000),                   # bs not a multiple of 128: unaligned blocks
     (4097, 300001),
@@ -127,10 +128,13 @@ def test_chunks_dev_vs_oracle(gpu, ctx, oracle, bs, nbytes):
     assert first_bad(got, want) is None, "block %s" % first_bad(got, want)
 
 
-@pytest.mark.parametrize("skew", [1, 4, 8, 15])
-def test_chunks_dev_misaligned_base(gpu, ctx, oracle, skew):
+@pytest.mark.parametrize("skew,nfull", [(1, 300), (4, 300), (8, 300), (15, 300), (4, 50000)])
+def test_chunks_dev_misaligned_base(gpu, ctx, oracle, skew, nfull):
+    """Quad mode (300 blocks) and lane mode (50000: the general loader, since
+    a misaligned base rules out the LDS-DMA body) on a misaligned file."""
     import torch
-    bs, nbytes = 32768, 300 * 32768 + 77
+    bs = 32768 if nfull < 1000 else 4096
+    nbytes = nfull * bs + 77
     data = dev_random(gpu, nbytes + skew, seed=skew)
     nb = (nbytes + bs - 1) // bs
     out = torch.zeros(nb * 32, dtype=torch.uint8, device="cuda:0")
@@ -602,3 +606,46 @@ def test_multi_device_split_paths(gpu, oracle, tmp_path):
     for block_size in (32768, 1024):
         cfg = gpu.ScannerConfig.new().block_size(block_size).threads(4).add_dir(str(tree), "/")
         assert gpu.v1.scan(cfg, context=ctx) == dirsig_oracle.scan(str(tree), block_size)
+
+
+def test_error_paths_are_codes_not_aborts(gpu, small_ctx, tmp_path):
+    """SURVEY.md 8b errors: bad arguments give CIR_EINVAL, unreadable sources
+    CIR_EIO (the reference's io::Error), never an abort; the context stays
+    usable afterwards."""
+    import torch
+    n = gpu._n
+    with pytest.raises(n.CiruelaError) as e:
+        small_ctx.hash_chunks_dev(0, 4096, 0, 0, 0)  # block_size 0
+    assert e.value.status == n.CIR_EINVAL
+    buf = torch.empty(4096 + 64, dtype=torch.uint8, device="cuda:0")
+    with pytest.raises(n.CiruelaError) as e:  # digests not 16-byte aligned
+        small_ctx.hash_chunks_dev(buf.data_ptr(), 4096, 1024, buf.data_ptr() + 8, 0)
+    assert e.value.status == n.CIR_EINVAL
+    with pytest.raises(n.CiruelaError) as e:
+        small_ctx.hash_memory(b"abc", 32768, gpu.HashType(77, "bogus"))  # unknown hash type
+    assert e.value.status == n.CIR_EINVAL
+    dfd = os.open(str(tmp_path), os.O_RDONLY)  # read() on a directory: EISDIR
+    try:
+        with pytest.raises(n.CiruelaError) as e:
+            small_ctx.hash_file(dfd, 32768)
+        assert e.value.status == n.CIR_EIO
+    finally:
+        os.close(dfd)
+    cfg = gpu.ScannerConfig.new().add_dir(str(tmp_path / "does-not-exist"), "/")
+    with pytest.raises(n.CiruelaError) as e:
+        gpu.v1.scan(cfg, context=small_ctx)
+    assert e.value.status == n.CIR_EIO
+    # still fine afterwards, on both the device and the host paths
+    data = os.urandom(100000)
+    want = b"".join(oracle_digest_any(data[i:i + 32768]) for i in range(0, len(data), 32768))
+    assert small_ctx.hash_memory(data, 32768) == want
+    t = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda:0")
+    out = torch.empty(32 * 4, dtype=torch.uint8, device="cuda:0")
+    small_ctx.hash_chunks_dev(t.data_ptr(), len(data), 32768, out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    assert out.cpu().numpy().tobytes() == want
+
+
+def oracle_digest_any(b):
+    import hashlib
+    return hashlib.blake2b(b, digest_size=32).digest()
