@@ -308,7 +308,7 @@ hipError_t launch_chain_step(uint64_t* st, const uint8_t* data, uint32_t n, bool
 
 // SHA-512/256 over a descriptor batch, one lane per block (dir-signature's
 // HashType::sha512_256()).
-__global__ __launch_bounds__(kThreads, 2) void k_sha_desc(const uint8_t* __restrict__ arena,
+__global__ __launch_bounds__(kThreads, 3) void k_sha_desc(const uint8_t* __restrict__ arena,
                                                            const uint64_t* __restrict__ off,
                                                            const uint32_t* __restrict__ len,
                                                            const uint32_t* __restrict__ perm,

@@ -243,14 +243,14 @@ __device__ __forceinline__ void chain(const uint8_t* p, uint64_t len, uint64_t h
 #pragma unroll
       for (int k = 0; k < 16; ++k) m[k] = 0;
     }
-    uint64_t w[16];
+    // big-endian words in place (the schedule reuses the same 16 registers)
 #pragma unroll
-    for (int k = 0; k < 16; ++k) w[k] = bswap64(m[k]);
+    for (int k = 0; k < 16; ++k) m[k] = bswap64(m[k]);
     if (bi + 1 == nblk) {
-      w[14] = len >> 61;
-      w[15] = len << 3;
+      m[14] = len >> 61;
+      m[15] = len << 3;
     }
-    compress(h, w);
+    compress(h, m);
   }
 }
 
