@@ -1,12 +1,23 @@
 // gfx950 kernels of the block-hash path.
 //
-//   k_uniform_glds   : the hot path.  nwaves x 64 equal blocks of bs bytes
-//                      (bs % 128 == 0, 16-byte aligned), one block chain per
+//   k_chunks         : the hot path (cir_hash_chunks_dev, >= kQuadSmallBatch
+//                      blocks): 64 equal blocks per wave, one block chain per
 //                      lane, message lines streamed HBM -> LDS by LDS-DMA
-//                      (global_load_lds_dwordx4) in full 128-byte lines.
+//                      (global_load_lds_dwordx4) in full 128-byte lines; the
+//                      ragged rest of the file in the same launch.
+//   k_uniform_glds   : the same body without the ragged rest (diagnostics).
 //   k_uniform_direct : same contract, each lane loads its own line straight
 //                      into VGPRs one line ahead (A/B variant of the loader).
+//   k_quad_chunks    : small files (< kQuadSmallBatch blocks): 4 lanes per
+//                      block chain, 16 chains per wave (DPP quad_perm).
+//   k_quad_long +
+//   k_lane_rest      : descriptor batches ordered longest chain first: long
+//                      chains in quad mode, the rest one lane per chain.
+//   k_chain_step     : the resumable single chain of the index footer.
 //   k_general        : ragged / misaligned blocks, chunk or descriptor form.
+//   k_sha_desc       : SHA-512/256 descriptors (dir-signature's 2nd hash).
+//   k_verify         : digest compare of the daemon-side batch verify.
+//   k_compress_only  : register-only compressions (live VALU ceiling).
 //   k_fill_splitmix64: synthetic test data (bench / tests only).
 //
 // Reference semantics: Hashes::hash_file's per-block split (dir-signature
