@@ -25,6 +25,9 @@ __global__ __launch_bounds__(256, 5) void k_mix(uint32_t* out, int iters) {
     if constexpr (K == 7) asm volatile(MIX_AsX ::: CLOBBERS);
     if constexpr (K == 8) asm volatile(MIX_As ::: CLOBBERS);
     if constexpr (K == 9) asm volatile(MIX_CX ::: CLOBBERS);
+    if constexpr (K == 10) asm volatile(MIX_A16X16 ::: CLOBBERS);
+    if constexpr (K == 11) asm volatile(MIX_A40X40 ::: CLOBBERS);
+    if constexpr (K == 12) asm volatile(MIX_A4X12 ::: CLOBBERS);
   }
   uint32_t v;
   asm volatile("v_mov_b32 %0, v10" : "=v"(v));
@@ -47,7 +50,10 @@ int main() {
       {"A8X8", k_mix<6>},
       {"AsX", k_mix<7>},
       {"As", k_mix<8>},
-      {"CX", k_mix<9>}
+      {"CX", k_mix<9>},
+      {"A16X16", k_mix<10>},
+      {"A40X40", k_mix<11>},
+      {"A4X12", k_mix<12>}
   };
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
