@@ -649,3 +649,58 @@ def test_error_paths_are_codes_not_aborts(gpu, small_ctx, tmp_path):
 def oracle_digest_any(b):
     import hashlib
     return hashlib.blake2b(b, digest_size=32).digest()
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_randomized_batches_and_files(gpu, ctx, oracle, seed):
+    """Seeded random shapes across every routing decision: descriptor batches
+    below and above the small-batch limit (49152), chain lengths around the
+    quad thresholds (8 and 1024 lines), misaligned offsets; device-resident
+    files with random block sizes (multiples of 128 or not) and block counts
+    on both sides of the limit."""
+    import torch
+    rng = random.Random(1000 + seed)
+    # descriptor batch
+    n = rng.choice([1, 7, 300, 5000, 49152, 49153, 60000])
+    lens = []
+    for _ in range(n):
+        kind = rng.random()
+        if kind < 0.5:
+            lens.append(rng.randrange(0, 4097))
+        elif kind < 0.8:
+            lens.append(rng.choice([1023, 1024, 1025, 8 * 128, 8 * 128 - 1, 32768]))
+        elif kind < 0.98:
+            lens.append(rng.randrange(4097, 200000))
+        else:
+            lens.append(rng.choice([1024 * 128 - 1, 1024 * 128, 1024 * 128 + 1, 1 << 20]))
+    offs, pos = [], 0
+    for ln in lens:
+        pos += rng.randrange(0, 17)
+        offs.append(pos)
+        pos += ln
+    data = dev_random(gpu, pos, seed=7 + seed)
+    d_off = torch.tensor(offs, dtype=torch.int64, device="cuda:0")
+    d_len = torch.tensor(lens, dtype=torch.int32, device="cuda:0")
+    out = torch.zeros(32 * n, dtype=torch.uint8, device="cuda:0")
+    ctx.hash_blocks_dev(data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    host = data.cpu().numpy()
+    ao = np.array(offs, dtype=np.uint64)
+    al = np.array(lens, dtype=np.uint32)
+    want = np.zeros(32 * n, dtype=np.uint8)
+    oracle.oracle_hash_blocks(host.ctypes.data, ao.ctypes.data, al.ctypes.data, n,
+                              want.ctypes.data, 8)
+    assert first_bad(out.cpu().numpy(), want) is None
+    del data, d_off, d_len, out
+    # device-resident file
+    bs = rng.choice([128 * rng.randrange(1, 64), rng.randrange(100, 9000)])
+    nblk = rng.choice([rng.randrange(1, 2000), rng.randrange(49000, 49300)])
+    nbytes = max(1, nblk * bs - rng.randrange(0, bs))
+    skew = rng.choice([0, 0, 16, 3])
+    fdata = dev_random(gpu, nbytes + skew, seed=99 + seed)
+    nb = (nbytes + bs - 1) // bs
+    fout = torch.zeros(nb * 32, dtype=torch.uint8, device="cuda:0")
+    ctx.hash_chunks_dev(fdata.data_ptr() + skew, nbytes, bs, fout.data_ptr(), 0)
+    torch.cuda.synchronize()
+    fh = fdata.cpu().numpy()[skew:].copy()
+    assert first_bad(fout.cpu().numpy(), oracle_chunks(oracle, fh, nbytes, bs)) is None
