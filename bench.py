@@ -58,6 +58,8 @@ def parse():
                    default="auto", help="auto = config2 at N=1, config4 at N>1")
     p.add_argument("--tree-gib", type=float, default=50.0, help="config5 tree size")
     p.add_argument("--host-gib", type=int, default=32, help="config2host buffer size")
+    p.add_argument("--staging-mib", type=int, default=0,
+                   help="staging buffer size of the host paths (0 = library default, 256)")
     p.add_argument("--tree-dir", default="/dev/shm/ciruela_bench_tree")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--force-dist", action="store_true",
@@ -370,7 +372,7 @@ def main():
     nblk = args.blocks
     nbytes = nblk * bs
     stream = torch.cuda.current_stream().cuda_stream
-    ctx = ca.Context(device_mask=1 << local)
+    ctx = ca.Context(device_mask=1 << local, staging_bytes=args.staging_mib << 20)
 
     if args.workload != "auto":
         if world != 1:
