@@ -51,6 +51,10 @@ hipError_t launch_order_desc(const uint32_t* len, uint64_t n, void* scratch, siz
                      quad_min_lines(n), key_in, idx_in, count);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  if (n == 1) {  // one chain (hash_bytes, an index footer): nothing to order
+    *perm = idx_in;
+    return hipSuccess;
+  }
   e = hipcub::DeviceRadixSort::SortPairsDescending(temp, temp_bytes, key_in, key_out, idx_in,
                                                    idx_out, (int)n, 0, 26, s);
   *perm = idx_out;
