@@ -116,3 +116,29 @@ def test_config3_full(gpu, oracle):
                               want.ctypes.data, THREADS)
     bad = np.nonzero((got != want).any(axis=1))[0]
     assert bad.size == 0, "blocks %s differ" % bad[:8]
+
+
+def test_quad_file_above_4gib(gpu, oracle):
+    """A device-resident file of 600 blocks of 8 MiB + 128 B (~5 GiB, a small
+    batch: quad mode) with a short last block: 64-bit offsets in the quad
+    path, every digest against the threaded oracle."""
+    import torch
+    bs = (8 << 20) + 128
+    nbytes = 600 * bs - 4321
+    seed = 0x5EED0006
+    data = torch.empty(nbytes + 8, dtype=torch.uint8, device="cuda:0")
+    gpu._n.check(gpu._n.lib.cir_fill_splitmix64_dev(data.data_ptr(), (nbytes + 7) // 8 * 8, seed,
+                                                    0, 0, 0))
+    nb = (nbytes + bs - 1) // bs
+    out = torch.empty(32 * nb, dtype=torch.uint8, device="cuda:0")
+    ctx = gpu.Context(device_mask=1)
+    ctx.hash_chunks_dev(data.data_ptr(), nbytes, bs, out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().reshape(-1, 32)
+    del data
+    host = np.empty((nbytes + 7) // 8, dtype=np.uint64)
+    host_fill(oracle, host, 0, seed)
+    want = np.zeros(32 * nb, dtype=np.uint8)
+    oracle.oracle_hash_chunks(host.ctypes.data, nbytes, bs, want.ctypes.data, THREADS)
+    bad = np.nonzero((got != want.reshape(-1, 32)).any(axis=1))[0]
+    assert bad.size == 0, "blocks %s differ" % bad[:8]
