@@ -444,6 +444,123 @@ __device__ __forceinline__ void g_quad(uint64_t& a, uint64_t& b, uint64_t& c, ui
   b = xor_rotr<63, 0>(b, c);
 }
 
+// The same G in hand-ordered asm (CIR_QUAD_ASM, the default): the permuted
+// b and c feed their 64-bit adds directly as VOP2 DPP carry pairs
+// (v_add_co_u32_dpp + v_addc_co_u32_dpp) and b's second read is a
+// v_xor_b32_dpp, so no value is moved across lanes on its own: 22 VALU
+// instructions per G instead of 24 (6-7 % less latency per compression,
+// tools/quad_dpp_ubench.hip).  One asm block is a whole compression
+// (compress_quad_asm, message words in registers) or a whole round
+// (round_quad_asm): the compiler puts an s_nop between two inline-asm blocks.
+// a, b, c, d, t (the rotr-32 result) and u (xor scratch) are pinned to
+// v[40:51] so that every block names the same registers; the compiler cannot
+// see the DPP reads inside the asm, so the blocks keep the DPP read-after-
+// write distance themselves: b is written by the last two instructions of a
+// step and first read across lanes by the third instruction of the next one
+// (2 wait states, the gfx9 DPP rule); c and d are read across lanes >= 5
+// instructions after their writes.  The last round ends with s_nop 1 for the
+// compiler-generated DPP reads of the finalisation.
+#ifndef CIR_QUAD_ASM
+#define CIR_QUAD_ASM 1
+#endif
+constexpr bool kQuadAsm = CIR_QUAD_ASM != 0;
+#define CIR_QP_39 " quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf"
+#define CIR_QP_4E " quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"
+#define CIR_QP_93 " quad_perm:[3,0,1,2] row_mask:0xf bank_mask:0xf"
+// second half of G (no cross-lane reads), shared by both forms
+#define CIR_QG_TAIL(Y)                                                        \
+  "v_lshl_add_u64 v[40:41], v[40:41], 0, " Y "\n"                             \
+  "v_lshl_add_u64 v[40:41], v[40:41], 0, v[42:43]\n"                          \
+  "v_xor_b32 v50, v48, v40\n"                                                 \
+  "v_xor_b32 v51, v49, v41\n"                                                 \
+  "v_alignbit_b32 v46, v51, v50, 16\n"                                        \
+  "v_alignbit_b32 v47, v50, v51, 16\n"                                        \
+  "v_lshl_add_u64 v[44:45], v[44:45], 0, v[46:47]\n"                          \
+  "v_xor_b32 v50, v42, v44\n"                                                 \
+  "v_xor_b32 v51, v43, v45\n"                                                 \
+  "v_alignbit_b32 v42, v50, v51, 31\n"                                        \
+  "v_alignbit_b32 v43, v51, v50, 31\n"
+// column step of round 0: every operand in its own lane
+#define CIR_QG_PLAIN(X, Y)                                                    \
+  "v_lshl_add_u64 v[40:41], v[40:41], 0, " X "\n"                             \
+  "v_lshl_add_u64 v[40:41], v[40:41], 0, v[42:43]\n"                          \
+  "v_xor_b32 v48, v47, v41\n"                                                 \
+  "v_xor_b32 v49, v46, v40\n"                                                 \
+  "v_lshl_add_u64 v[44:45], v[44:45], 0, v[48:49]\n"                          \
+  "v_xor_b32 v50, v42, v44\n"                                                 \
+  "v_xor_b32 v51, v43, v45\n"                                                 \
+  "v_alignbit_b32 v42, v51, v50, 24\n"                                        \
+  "v_alignbit_b32 v43, v50, v51, 24\n" CIR_QG_TAIL(Y)
+// b from lane PB, c from lane PC, d from lane PD
+#define CIR_QG_DPP(PB, PC, PD, X, Y)                                          \
+  "v_lshl_add_u64 v[40:41], v[40:41], 0, " X "\n"                             \
+  "v_add_co_u32_dpp v40, vcc, v42, v40" PB "\n"                               \
+  "v_addc_co_u32_dpp v41, vcc, v43, v41, vcc" PB "\n"                         \
+  "v_xor_b32_dpp v48, v47, v41" PD "\n"                                       \
+  "v_xor_b32_dpp v49, v46, v40" PD "\n"                                       \
+  "v_add_co_u32_dpp v44, vcc, v44, v48" PC "\n"                               \
+  "v_addc_co_u32_dpp v45, vcc, v45, v49, vcc" PC "\n"                         \
+  "v_xor_b32_dpp v50, v42, v44" PB "\n"                                       \
+  "v_xor_b32_dpp v51, v43, v45" PB "\n"                                       \
+  "v_alignbit_b32 v42, v51, v50, 24\n"                                        \
+  "v_alignbit_b32 v43, v50, v51, 24\n" CIR_QG_TAIL(Y)
+// diagonal step: b, c, d from lanes i+1, i+2, i+3; column step (rounds >= 1):
+// back from lanes i+3, i+2, i+1
+#define CIR_QG_DIAG CIR_QG_DPP(CIR_QP_39, CIR_QP_4E, CIR_QP_93, "%[x1]", "%[y1]")
+#define CIR_QG_COL CIR_QG_DPP(CIR_QP_93, CIR_QP_4E, CIR_QP_39, "%[x0]", "%[y0]")
+#define CIR_QG_OPS                                                            \
+  : "+{v[40:41]}"(a), "+{v[42:43]}"(b), "+{v[44:45]}"(c), "+{v[46:47]}"(d),   \
+    "=&{v[48:49]}"(t), "=&{v[50:51]}"(u)                                      \
+  : [x0] "v"(x0), [y0] "v"(y0), [x1] "v"(x1), [y1] "v"(y1)                    \
+  : "vcc"
+
+// Whole compression in one block (message words prefetched into registers:
+// no s_nop between rounds).  Word k of the schedule is operand m(k mod 40):
+// rounds 10 and 11 repeat rounds 0 and 1.
+#define CIR_M(k) "%[m" #k "]"
+#define CIR_QR(K0, K1, K2, K3)                                                \
+  CIR_QG_DPP(CIR_QP_93, CIR_QP_4E, CIR_QP_39, CIR_M(K0), CIR_M(K1))           \
+  CIR_QG_DPP(CIR_QP_39, CIR_QP_4E, CIR_QP_93, CIR_M(K2), CIR_M(K3))
+#define CIR_QCOMPRESS                                                         \
+  CIR_QG_PLAIN(CIR_M(0), CIR_M(1))                                            \
+  CIR_QG_DPP(CIR_QP_39, CIR_QP_4E, CIR_QP_93, CIR_M(2), CIR_M(3))             \
+  CIR_QR(4, 5, 6, 7) CIR_QR(8, 9, 10, 11) CIR_QR(12, 13, 14, 15)              \
+  CIR_QR(16, 17, 18, 19) CIR_QR(20, 21, 22, 23) CIR_QR(24, 25, 26, 27)        \
+  CIR_QR(28, 29, 30, 31) CIR_QR(32, 33, 34, 35) CIR_QR(36, 37, 38, 39)        \
+  CIR_QR(0, 1, 2, 3) CIR_QR(4, 5, 6, 7) "s_nop 1\n"
+#define CIR_MO(k) [m##k] "v"(m[k])
+
+__device__ __forceinline__ void compress_quad_asm(uint64_t& a, uint64_t& b, uint64_t& c,
+                                                  uint64_t& d, const uint64_t (&m)[40]) {
+  uint64_t t, u;
+  asm volatile(CIR_QCOMPRESS
+               : "+{v[40:41]}"(a), "+{v[42:43]}"(b), "+{v[44:45]}"(c), "+{v[46:47]}"(d),
+                 "=&{v[48:49]}"(t), "=&{v[50:51]}"(u)
+               : CIR_MO(0), CIR_MO(1), CIR_MO(2), CIR_MO(3), CIR_MO(4), CIR_MO(5), CIR_MO(6),
+                 CIR_MO(7), CIR_MO(8), CIR_MO(9), CIR_MO(10), CIR_MO(11), CIR_MO(12),
+                 CIR_MO(13), CIR_MO(14), CIR_MO(15), CIR_MO(16), CIR_MO(17), CIR_MO(18),
+                 CIR_MO(19), CIR_MO(20), CIR_MO(21), CIR_MO(22), CIR_MO(23), CIR_MO(24),
+                 CIR_MO(25), CIR_MO(26), CIR_MO(27), CIR_MO(28), CIR_MO(29), CIR_MO(30),
+                 CIR_MO(31), CIR_MO(32), CIR_MO(33), CIR_MO(34), CIR_MO(35), CIR_MO(36),
+                 CIR_MO(37), CIR_MO(38), CIR_MO(39)
+               : "vcc");
+}
+
+// One round of quad mode: column step (words x0, y0), diagonal step (x1, y1).
+// kFirst: round 0 (state in the column layout); kLast: round 11.
+template <bool kFirst, bool kLast>
+__device__ __forceinline__ void round_quad_asm(uint64_t& a, uint64_t& b, uint64_t& c,
+                                               uint64_t& d, uint64_t x0, uint64_t y0,
+                                               uint64_t x1, uint64_t y1) {
+  uint64_t t, u;
+  if constexpr (kFirst)
+    asm volatile(CIR_QG_PLAIN("%[x0]", "%[y0]") CIR_QG_DIAG CIR_QG_OPS);
+  else if constexpr (kLast)
+    asm volatile(CIR_QG_COL CIR_QG_DIAG "s_nop 1\n" CIR_QG_OPS);
+  else
+    asm volatile(CIR_QG_COL CIR_QG_DIAG CIR_QG_OPS);
+}
+
 // One compression of the chain owned by this quad.  line = the quad's 128-B
 // message line in LDS; addr[r*4 + k] = byte offset of the k-th word lane i
 // needs in round r.  cv/dv = IV[i]/IV[4+i]; dmask = this lane's t / final-flag
@@ -453,7 +570,7 @@ __device__ __forceinline__ void g_quad(uint64_t& a, uint64_t& b, uint64_t& c, ui
 // or not it depends on the previous one (tools/lat_ubench.hip), so the
 // latency of a chain is its instruction count: 20 per G + 4 permutes per
 // layout change, the finalisation reading c, b, d across lanes.
-template <bool kPrefetchAll>
+template <bool kPrefetchAll, bool kAsm = kQuadAsm>
 __device__ __forceinline__ void compress_quad_t(uint64_t& h0, uint64_t& h1, const uint8_t* line,
                                                 const uint32_t (&addr)[48], uint64_t cv,
                                                 uint64_t dv) {
@@ -475,14 +592,25 @@ __device__ __forceinline__ void compress_quad_t(uint64_t& h0, uint64_t& h1, cons
     else
       return *reinterpret_cast<const uint64_t*>(line + addr[k]);
   };
-  g_quad<0, 0, 0>(a, b, c, d, word(0), word(1));
-  g_quad<kQuadFromNext, kQuadFromNext2, kQuadFromPrev>(a, b, c, d, word(2), word(3));
+  if constexpr (kAsm && kPrefetchAll) {
+    compress_quad_asm(a, b, c, d, msg);
+  } else if constexpr (kAsm) {
+    round_quad_asm<true, false>(a, b, c, d, word(0), word(1), word(2), word(3));
 #pragma unroll
-  for (int r = 1; r < 12; ++r) {
-    g_quad<kQuadFromPrev, kQuadFromNext2, kQuadFromNext>(a, b, c, d, word(4 * r + 0),
-                                                         word(4 * r + 1));
-    g_quad<kQuadFromNext, kQuadFromNext2, kQuadFromPrev>(a, b, c, d, word(4 * r + 2),
-                                                         word(4 * r + 3));
+    for (int r = 1; r < 11; ++r)
+      round_quad_asm<false, false>(a, b, c, d, word(4 * r), word(4 * r + 1), word(4 * r + 2),
+                                   word(4 * r + 3));
+    round_quad_asm<false, true>(a, b, c, d, word(44), word(45), word(46), word(47));
+  } else {
+    g_quad<0, 0, 0>(a, b, c, d, word(0), word(1));
+    g_quad<kQuadFromNext, kQuadFromNext2, kQuadFromPrev>(a, b, c, d, word(2), word(3));
+#pragma unroll
+    for (int r = 1; r < 12; ++r) {
+      g_quad<kQuadFromPrev, kQuadFromNext2, kQuadFromNext>(a, b, c, d, word(4 * r + 0),
+                                                           word(4 * r + 1));
+      g_quad<kQuadFromNext, kQuadFromNext2, kQuadFromPrev>(a, b, c, d, word(4 * r + 2),
+                                                           word(4 * r + 3));
+    }
   }
   // back to the column layout inside the finalisation: c_i from lane i+2,
   // b_i from lane i+3, d_i from lane i+1
@@ -496,6 +624,27 @@ __device__ __forceinline__ void compress_quad(uint64_t& h0, uint64_t& h1, const 
                                               const uint32_t (&addr)[48], uint64_t cv,
                                               uint64_t dv) {
   compress_quad_t<false>(h0, h1, line, addr, cv, dv);
+}
+
+// Software-pipelined quad mode (quad_run's asm path): the 40 message words
+// of line k+1 are read from LDS into a second register set while line k
+// compresses, so a compression never waits on the LDS round trip (write,
+// 40 reads, ~300-500 cycles for a wave alone).
+__device__ __forceinline__ void quad_read_msg(uint64_t (&m)[40], const uint8_t* line,
+                                              const uint32_t (&addr)[48]) {
+#pragma unroll
+  for (int k = 0; k < 40; ++k) m[k] = *reinterpret_cast<const uint64_t*>(line + addr[k]);
+}
+
+__device__ __forceinline__ void compress_quad_regs(uint64_t& h0, uint64_t& h1,
+                                                   const uint64_t (&m)[40], uint64_t cv,
+                                                   uint64_t dv) {
+  uint64_t a = h0, b = h1, c = cv, d = dv;
+  compress_quad_asm(a, b, c, d, m);
+  const uint64_t cc = mk64(qd<kQuadFromNext2>(lo32(c)) ^ lo32(a), qd<kQuadFromNext2>(hi32(c)) ^ hi32(a));
+  h0 = h0 ^ cc;
+  const uint64_t bb = mk64(qd<kQuadFromPrev>(lo32(b)) ^ lo32(h1), qd<kQuadFromPrev>(hi32(b)) ^ hi32(h1));
+  h1 = mk64(qd<kQuadFromNext>(lo32(d)) ^ lo32(bb), qd<kQuadFromNext>(hi32(d)) ^ hi32(bb));
 }
 
 // Bytes [32k, 32k + 32) of a line at p, of which the first n (0..32) are

@@ -171,7 +171,7 @@ __device__ __forceinline__ void quad_init(uint32_t i, uint64_t& h0, uint64_t& h1
 // Advance a quad's chain over L bytes at p, t0 bytes already compressed.
 // final: the last line (partial, or the empty block of an empty input)
 // carries the final flag; otherwise L must be a multiple of 128.
-template <bool kPrefetchAll = false>
+template <bool kPrefetchAll = false, bool kAsm = kQuadAsm>
 __device__ __forceinline__ void quad_run(uint64_t& h0, uint64_t& h1, uint64_t t0,
                                          const uint8_t* p, uint32_t L, bool active, bool final,
                                          uint8_t* lds, const uint32_t (&addr)[48], uint32_t line,
@@ -188,6 +188,40 @@ __device__ __forceinline__ void quad_run(uint64_t& h0, uint64_t& h1, uint64_t t0
   };
   uint4 u = make_uint4(0, 0, 0, 0), w = u;
   if (total) fetch(0, u, w);
+  if constexpr (kAsm && kPrefetchAll) {
+    // Pipelined: line it+1 goes regs -> LDS -> the other message set (ma /
+    // mb) while line it compresses.  At the top of each half the previous
+    // reads have landed (lgkmcnt(0)), so the LDS line is free for the next
+    // write and the asm's operands need no wait; the next set's 40 reads
+    // stay in flight across the compression (the asm names only the current
+    // set).  A compression no longer waits on the LDS round trip (write, 40
+    // reads: ~300-500 cycles for a wave alone).
+    uint64_t ma[40], mb[40];
+    auto stage = [&](uint32_t it, uint64_t (&m)[40]) {
+      *reinterpret_cast<uint4*>(lds + line + 32u * i) = u;
+      *reinterpret_cast<uint4*>(lds + line + 32u * i + 16u) = w;
+      if (it + 1 < total) fetch(it + 1, u, w);
+      quad_read_msg(m, lds, addr);
+    };
+    auto step = [&](uint32_t it, const uint64_t (&m)[40]) {
+      const bool last = final && it + 1 == total;
+      const uint64_t t = t0 + (last ? (uint64_t)L : (uint64_t)(it + 1) * 128u);
+      const uint64_t dv = dv0 ^ (i == 0 ? t : 0ull) ^ ((i == 2 && last) ? ~0ull : 0ull);
+      compress_quad_regs(h0, h1, m, cv, dv);
+    };
+    constexpr int kLgkm0 = 0xC07F;  // s_waitcnt lgkmcnt(0), vmcnt/expcnt untouched
+    if (total) stage(0, ma);
+    for (uint32_t it = 0; it < total; it += 2) {
+      __builtin_amdgcn_s_waitcnt(kLgkm0);
+      if (it + 1 < total) stage(it + 1, mb);
+      step(it, ma);
+      if (it + 1 >= total) break;
+      __builtin_amdgcn_s_waitcnt(kLgkm0);
+      if (it + 2 < total) stage(it + 2, ma);
+      step(it + 1, mb);
+    }
+    return;
+  }
   for (uint32_t it = 0; it < total; ++it) {
     // publish this lane's 32 bytes of the line to its quad (LDS is in order
     // per wave: the previous compression's reads precede these writes)
@@ -197,13 +231,13 @@ __device__ __forceinline__ void quad_run(uint64_t& h0, uint64_t& h1, uint64_t t0
     const bool last = final && it + 1 == total;
     const uint64_t t = t0 + (last ? (uint64_t)L : (uint64_t)(it + 1) * 128u);
     const uint64_t dv = dv0 ^ (i == 0 ? t : 0ull) ^ ((i == 2 && last) ? ~0ull : 0ull);
-    compress_quad_t<kPrefetchAll>(h0, h1, lds, addr, cv, dv);
+    compress_quad_t<kPrefetchAll, kAsm>(h0, h1, lds, addr, cv, dv);
   }
 }
 
 // The chain of quad q of this wave (block b at p, L bytes; have = false for a
 // quad past the end) is hashed into out + 32 b.
-template <bool kPrefetchAll>
+template <bool kPrefetchAll, bool kAsm = kQuadAsm>
 __device__ __forceinline__ void quad_chain(bool have, uint64_t b, const uint8_t* p, uint32_t L,
                                            uint8_t* __restrict__ out, uint8_t* lds,
                                            uint32_t wave_lds) {
@@ -213,11 +247,11 @@ __device__ __forceinline__ void quad_chain(bool have, uint64_t b, const uint8_t*
   quad_addr(addr, line, i);
   uint64_t h0, h1;
   quad_init(i, h0, h1);
-  quad_run<kPrefetchAll>(h0, h1, 0, p, have ? L : 0u, have, true, lds, addr, line, i);
+  quad_run<kPrefetchAll, kAsm>(h0, h1, 0, p, have ? L : 0u, have, true, lds, addr, line, i);
   if (have) *reinterpret_cast<uint64_t*>(out + b * 32u + 8u * i) = h0;
 }
 
-template <bool kPrefetchAll>
+template <bool kPrefetchAll, bool kAsm>
 __device__ __forceinline__ void quad_chains(const uint8_t* __restrict__ arena,
                                             const uint64_t* __restrict__ off,
                                             const uint32_t* __restrict__ len,
@@ -233,7 +267,7 @@ __device__ __forceinline__ void quad_chains(const uint8_t* __restrict__ arena,
     o = off[b];
     L = len[b];
   }
-  quad_chain<kPrefetchAll>(have, b, arena + o, L, out, lds, wave_lds);
+  quad_chain<kPrefetchAll, kAsm>(have, b, arena + o, L, out, lds, wave_lds);
 }
 
 // Hashes::hash_file split of one device-resident file with fewer than
@@ -258,6 +292,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))
 // Latency-bound (one 1 MiB chain = 8192 dependent compressions), so it reads
 // each line's 48 message words up front (176 VGPRs) and runs at s_setprio 3;
 // it is its own kernel so the lane part keeps its occupancy.
+template <bool kAsm>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_quad_long(
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ perm, const uint32_t* n_long,
@@ -268,7 +303,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))
   const uint32_t first = (blockIdx.x * kWaves + wave) * 16u;
   if (first >= nl) return;
   __builtin_amdgcn_s_setprio(3);
-  quad_chains<true>(arena, off, len, perm, first, nl, out, lds, wave * kQuadWaveLds);
+  quad_chains<true, kAsm>(arena, off, len, perm, first, nl, out, lds, wave * kQuadWaveLds);
 }
 
 // Lane part: chains [nl, n) of the order, one lane per chain.
@@ -483,8 +518,8 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
                      len, perm, n, n_long, (uint32_t)nq, out);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_quad_long, dim3((unsigned)nq), dim3(kThreads), 0, s, arena, off, len, perm,
-                     n_long, (uint32_t)nq, out);
+  hipLaunchKernelGGL(k_quad_long<kQuadAsm>, dim3((unsigned)nq), dim3(kThreads), 0, s, arena, off,
+                     len, perm, n_long, (uint32_t)nq, out);
   e = hipGetLastError();
   if (e == hipSuccess) e = hipEventRecord(join, aux);
   if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);

@@ -29,7 +29,10 @@ constexpr int kQuadMaxWg = 256;  // at most 256 x 64 = 16384 chains in quad mode
 // chains (within 4 % there at 32 KiB, 256 KiB and 1 MiB); at 65535 lane
 // mode is ahead (1548 vs 1335 GiB/s at 32 KiB, 1928 vs 1567 at 256 KiB;
 // profiles/r01/shapes.log).
-constexpr uint64_t kQuadSmallBatch = 49153;
+#ifndef CIR_QUAD_SMALL_BATCH
+#define CIR_QUAD_SMALL_BATCH 49153
+#endif
+constexpr uint64_t kQuadSmallBatch = CIR_QUAD_SMALL_BATCH;
 constexpr uint32_t kQuadSmallMinLines = 8;
 inline uint32_t quad_min_lines(uint64_t n) {
   return n < kQuadSmallBatch ? kQuadSmallMinLines : kQuadMinLines;

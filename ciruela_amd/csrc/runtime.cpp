@@ -615,13 +615,13 @@ int cir_hash_blocks_ht(cir_ctx* ctx, int hash_type, const uint8_t* h_arena, cons
   // contiguous ranges balanced by bytes
   const size_t nd = std::min(ctx->devs.size(), nblk);
   uint64_t total = 0;
-  for (size_t i = 0; i < nblk; ++i) total += len[i] + 128;
+  for (size_t i = 0; i < nblk; ++i) total += (uint64_t)len[i] + 128;
   std::vector<size_t> cut(nd + 1, nblk);
   cut[0] = 0;
   uint64_t acc = 0;
   size_t p = 1;
   for (size_t i = 0; i < nblk && p < nd; ++i) {
-    acc += len[i] + 128;
+    acc += (uint64_t)len[i] + 128;
     if (acc * nd >= total * p) cut[p++] = i + 1;
   }
   return for_each_device(ctx, [&](Device& d, size_t i) {

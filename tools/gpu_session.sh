@@ -29,6 +29,9 @@ for s in "$@"; do
     ablib)
       step ablib 600 python tools/ab_lib.py abtest/*.so > gpurun_out/ablib.log 2>&1
       cat gpurun_out/ablib.log ;;
+    abquad)
+      step abquad 600 python tools/ab_quad.py abtest/*.so > gpurun_out/abquad.log 2>&1
+      cat gpurun_out/abquad.log ;;
     h2d)
       step h2d 300 python tools/h2d_probe.py > gpurun_out/h2d.log 2>&1
       HSA_ENABLE_SDMA=0 step h2d_blit 300 python tools/h2d_probe.py > gpurun_out/h2d_blit.log 2>&1
@@ -105,6 +108,15 @@ for s in "$@"; do
         step "bs$1" 300 python bench.py --block-size $1 --blocks $2 --steps 5 --warmup 1 --no-cpu-baseline \
           > gpurun_out/shape.json 2> gpurun_out/shape.err
         echo "bs=$1 nblk=$2 $(grep -o '"value": [0-9.]*' gpurun_out/shape.json) $(grep -o '"kernel_ms_avg": [0-9.]*' gpurun_out/shape.json)"
+      done ;;
+    shapesab)  # SHAPES over every abtest/*.so (CIRUELA_AMD_LIB), chunk form
+      for sh in ${SHAPES:-32768_16384 32768_32768 32768_49152 32768_65535 32768_98304 1048576_16384 1048576_32768 262144_65535}; do
+        set -- ${sh/_/ }
+        for lib in abtest/*.so; do
+          CIRUELA_AMD_LIB=$PWD/$lib step "bs$1" 300 python bench.py --block-size $1 --blocks $2 --steps 5 \
+            --warmup 1 --no-cpu-baseline > gpurun_out/shape.json 2> gpurun_out/shape.err
+          echo "bs=$1 nblk=$2 $lib $(grep -o '"value": [0-9.]*' gpurun_out/shape.json)"
+        done
       done ;;
     cfg1)
       step cfg1 300 python bench.py --workload config1 > gpurun_out/cfg1.json 2> gpurun_out/cfg1.err
