@@ -31,6 +31,10 @@
 #include "uniform.hpp"
 #include "sha512_dev.hpp"
 
+#ifndef CIR_QUAD_EXCLUSIVE
+#define CIR_QUAD_EXCLUSIVE 1
+#endif
+
 namespace cir {
 namespace dev {
 
@@ -289,21 +293,29 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))
 }
 
 // Quad part of an ordered batch: chains [0, nl), nl = min(*n_long, 64 nq_wg).
-// Latency-bound (one 1 MiB chain = 8192 dependent compressions), so it reads
-// each line's 48 message words up front (176 VGPRs) and runs at s_setprio 3;
-// it is its own kernel so the lane part keeps its occupancy.
-template <bool kAsm>
+// Latency-bound (one 1 MiB chain = 8192 dependent compressions), so it keeps
+// a line's 40 message words in registers and runs at s_setprio 3; it is its
+// own kernel so the lane part keeps its occupancy.  kExclusive: each wave
+// touches a255, so it holds the SIMD's whole 512-register file and no lane
+// wave can share its SIMD (batches with a lane part beside the quad part).
+template <bool kAsm, bool kExclusive>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_quad_long(
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ perm, const uint32_t* n_long,
     uint32_t nq_wg, uint8_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWaves * kQuadWaveLds];
+  if constexpr (kExclusive) asm volatile("v_accvgpr_write_b32 a255, 0" ::: "a255");
   const uint32_t nl = min(*n_long, nq_wg * 64u);
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t first = (blockIdx.x * kWaves + wave) * 16u;
   if (first >= nl) return;
   __builtin_amdgcn_s_setprio(3);
   quad_chains<true, kAsm>(arena, off, len, perm, first, nl, out, lds, wave * kQuadWaveLds);
+}
+
+// A bounded pause on a stream: `rounds` x s_sleep 127 (~3.4 us each).
+__global__ void k_delay(uint32_t rounds) {
+  for (uint32_t r = 0; r < rounds; ++r) __builtin_amdgcn_s_sleep(127);
 }
 
 // Lane part: chains [nl, n) of the order, one lane per chain.
@@ -511,15 +523,31 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
   const uint64_t nq = std::min<uint64_t>((n + 63) / 64, quad_max_wg(n));
   const uint64_t lane_grid = grid_for(n, kThreads);
   if (lane_grid > 0x7fffffffull) return hipErrorInvalidValue;
+  const bool exclusive = CIR_QUAD_EXCLUSIVE && n >= kQuadSmallBatch;
   hipError_t e = hipEventRecord(fork, s);
   if (e == hipSuccess) e = hipStreamWaitEvent(aux, fork, 0);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads), 0, aux, arena, off,
-                     len, perm, n, n_long, (uint32_t)nq, out);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_quad_long<kQuadAsm>, dim3((unsigned)nq), dim3(kThreads), 0, s, arena, off,
-                     len, perm, n_long, (uint32_t)nq, out);
+  if (exclusive) {
+    // The quad workgroups need whole CUs (one 504-register wave per SIMD):
+    // they are dispatched first, and the lane part starts ~20 us later, so
+    // its waves fill the other CUs instead of taking every SIMD first.
+    hipLaunchKernelGGL((k_quad_long<kQuadAsm, true>), dim3((unsigned)nq), dim3(kThreads), 0, s,
+                       arena, off, len, perm, n_long, (uint32_t)nq, out);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, aux, 6u);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads), 0, aux, arena, off,
+                       len, perm, n, n_long, (uint32_t)nq, out);
+  } else {
+    hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads), 0, aux, arena, off,
+                       len, perm, n, n_long, (uint32_t)nq, out);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_quad_long<kQuadAsm, false>), dim3((unsigned)nq), dim3(kThreads), 0, s,
+                       arena, off, len, perm, n_long, (uint32_t)nq, out);
+  }
   e = hipGetLastError();
   if (e == hipSuccess) e = hipEventRecord(join, aux);
   if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
