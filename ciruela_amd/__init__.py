@@ -102,6 +102,8 @@ class Context:
         for o, ln in zip(offsets, lengths):
             if o < 0 or ln < 0 or o + ln > len(arena):
                 raise ValueError("block outside the arena")
+            if ln > 0xFFFFFFFF:
+                raise ValueError("block longer than 2^32 - 1 bytes")
         out = ctypes.create_string_buffer(32 * max(n, 1))
         if n == 0:
             return b""
@@ -144,6 +146,8 @@ class Context:
         for o, ln in zip(offsets, lengths):
             if o < 0 or ln < 0 or o + ln > len(arena):
                 raise ValueError("block outside the arena")
+            if ln > 0xFFFFFFFF:
+                raise ValueError("block longer than 2^32 - 1 bytes")
         if n == 0:
             return []
         offs = (ctypes.c_uint64 * n)(*offsets)

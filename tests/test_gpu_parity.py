@@ -194,6 +194,39 @@ def test_desc_mixed_ragged_shuffled(gpu, ctx, oracle):
     assert first_bad(out.cpu().numpy(), want) is None
 
 
+def test_desc_large_batch_exclusive_quad(gpu, ctx, oracle):
+    """A batch above the small-batch limit (>= 49153 descriptors) with long
+    chains: the quad part runs SIMD-exclusive (k_quad_long<_, true>, launched
+    before a delayed lane part), the rest in lane mode; chain lengths on both
+    sides of the 1024-line threshold, odd and even line counts, ragged
+    tails, 16-B aligned and misaligned starts."""
+    import torch
+    rng = random.Random(0xE5C1)
+    q = 1024 * 128
+    lens = [rng.choice([q - 128, q - 1, q, q + 1, q + 128, 2 * q + 77, 3 * q]) for _ in range(150)]
+    lens += [rng.randrange(0, 8192) for _ in range(50000)]
+    rng.shuffle(lens)
+    offs, pos = [], 0
+    for i, ln in enumerate(lens):
+        pos += (-pos) % 16 + (3 if i % 11 == 0 else 0)
+        offs.append(pos)
+        pos += ln
+    data = dev_random(gpu, pos, seed=41)
+    d_off = torch.tensor(offs, dtype=torch.int64, device="cuda:0")
+    d_len = torch.tensor(lens, dtype=torch.int32, device="cuda:0")
+    out = torch.zeros(32 * len(lens), dtype=torch.uint8, device="cuda:0")
+    ctx.hash_blocks_dev(data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), len(lens),
+                        out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    host = data.cpu().numpy()
+    ao = np.array(offs, dtype=np.uint64)
+    al = np.array(lens, dtype=np.uint32)
+    want = np.zeros(32 * len(lens), dtype=np.uint8)
+    oracle.oracle_hash_blocks(host.ctypes.data, ao.ctypes.data, al.ctypes.data, len(lens),
+                              want.ctypes.data, 8)
+    assert first_bad(out.cpu().numpy(), want) is None
+
+
 def test_host_blocks_many_batches(small_ctx, oracle):
     rng = random.Random(11)
     arena = os.urandom(6 << 20)
