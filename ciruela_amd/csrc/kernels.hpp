@@ -24,11 +24,11 @@ constexpr int kQuadMaxWg = 256;  // at most 256 x 64 = 16384 chains in quad mode
 // (64 x 1024 = 65536 chains; lane mode measured 2232 GiB/s at 8 M x 4 KiB
 // but 1024 GiB/s at 32 K x 1 MiB and 258 at 8 K x 4 MiB).  Batches of at
 // most 49152 chains run every chain of at least kQuadSmallMinLines lines in
-// quad mode (4 x the waves, ~1/3 the latency per compression): 1537-1638
-// GiB/s at 32 K x 1 MiB, 737 at 8 K x 4 MiB.  The two modes cross at ~49152
-// chains (within 4 % there at 32 KiB, 256 KiB and 1 MiB); at 65535 lane
-// mode is ahead (1548 vs 1335 GiB/s at 32 KiB, 1928 vs 1567 at 256 KiB;
-// profiles/r01/shapes.log).
+// quad mode (4 x the waves, ~1/3 the latency per compression): 1648-1700
+// GiB/s at 32 K x 1 MiB, 757-784 at 8 K x 4 MiB (asm quad G).  The two
+// modes cross at ~49152 chains (within 4 % there at 32 KiB, 256 KiB and
+// 1 MiB); at 65535 lane mode is ahead (1606 vs 1438 GiB/s at 32 KiB, 1916
+// vs 1703 at 256 KiB; profiles/r01/quad_asm_ab.md).
 #ifndef CIR_QUAD_SMALL_BATCH
 #define CIR_QUAD_SMALL_BATCH 49153
 #endif
