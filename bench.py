@@ -366,7 +366,19 @@ def main():
     dev = torch.device("cuda", local)
     distributed = world > 1 or args.force_dist
     if distributed:
-        dist.init_process_group("nccl", device_id=dev)
+        # RCCL prints its version banner on stdout when the communicator
+        # comes up; keep stdout for the one JSON line (fd-level, so the C
+        # library's writes go to stderr too).
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("nccl", device_id=dev)
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
 
     bs = args.block_size
     nblk = args.blocks

@@ -11,12 +11,12 @@ export TMPDIR=/tmp
 step() {  # name timeout cmd...
   local name=$1 t=$2
   shift 2
-  echo "== $name: $*"
+  echo "== $name: $*" >&2
   timeout -k 10 "$t" "$@"
   local rc=$?
-  echo "== $name rc=$rc"
+  echo "== $name rc=$rc" >&2
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
-    echo "== stopping after $name (rc=$rc)"
+    echo "== stopping after $name (rc=$rc)" >&2
     exit $rc
   fi
   return 0
