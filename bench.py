@@ -62,6 +62,9 @@ def parse():
                    help="staging buffer size of the host paths (0 = library default, 256)")
     p.add_argument("--tree-dir", default="/dev/shm/ciruela_bench_tree")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                   help="process group of the N>1 path (nccl = RCCL; gloo for rehearsals "
+                        "with several ranks per GPU)")
     p.add_argument("--force-dist", action="store_true",
                    help="run the N>1 code path (process group, config 4) even at world size 1")
     p.add_argument("--cpu-seconds", type=float, default=2.5,
@@ -93,51 +96,144 @@ def load_traffic(cfg_key):
         return None
 
 
+def load_oracle():
+    """The C oracle (test infrastructure): the CPU baseline and the checker
+    of the secondary legs, never the measured path."""
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "liboracle_blake2b.so"))
+    vp, u64 = ctypes.c_void_p, ctypes.c_uint64
+    lib.oracle_hash_chunks.argtypes = [vp, u64, u64, vp, ctypes.c_int]
+    lib.oracle_hash_blocks.argtypes = [vp, vp, vp, ctypes.c_size_t, vp, ctypes.c_int]
+    lib.oracle_splitmix64_fill.argtypes = [vp, u64, u64, u64, u64, u64]
+    return lib
+
+
+# CPU share of one GPU on the measurement boxes: gpurun gives a one-GPU box
+# 16 host CPUs (OMP_NUM_THREADS / MAX_JOBS are set to 16 there) while
+# os.cpu_count() and the affinity mask show the whole host.  "All cores" of
+# the CPU baseline is therefore min(affinity, 16); host_info() records both.
+CPU_SHARE_PER_GPU = 16
+
+
+def host_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            "cpu_model": model, "cpu_share_per_gpu": CPU_SHARE_PER_GPU}
+
+
+def all_cores():
+    return max(1, min(CPU_SHARE_PER_GPU, len(os.sched_getaffinity(0))))
+
+
+def cpu_rates(run, target_s):
+    """run(threads) -> bytes hashed by one pass over the sample; repeated
+    until `target_s` wall seconds at 4 threads (the same CPU work, so
+    target_s * 4 / threads, at more threads).  {threads: (GiB/s, bytes)}."""
+    res = {}
+    for threads in sorted({4, all_cores()}):
+        wall = target_s * 4.0 / threads if threads > 4 else target_s
+        done, t0 = 0, time.perf_counter()
+        while True:
+            done += run(threads)
+            dt = time.perf_counter() - t0
+            if dt >= wall:
+                break
+        res[threads] = (done / dt / GIB, done)
+    return res
+
+
+def cpu_record(res, sample, unit="GiB/s"):
+    t4, ac = res[4], res[all_cores()]
+    return {"value": round(t4[0], 4), "unit": unit, "cores": 4, "kind": "port",
+            "sample": sample,
+            "all_cores": {"value": round(ac[0], 4), "cores": all_cores(),
+                          "sample_bytes": ac[1]},
+            "host": host_info()}
+
+
 def cpu_baseline(bs, target_s):
     """Oracle BLAKE2b-256 over config-2 blocks on the host (bounded sample)."""
     import numpy as np
-    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "liboracle_blake2b.so"))
-    lib.oracle_hash_chunks.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
-                                       ctypes.c_void_p, ctypes.c_int]
-    lib.oracle_splitmix64_fill.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
-                                           ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
-    all_cores = max(1, min(16, len(os.sched_getaffinity(0))))
-
-    # one sample buffer (config-2 bytes of blocks 32.., 4 GiB at most), hashed
-    # over and over until the measurement has run its share of the ~25 s of
-    # CPU work (4 threads ~2.5 s wall, all cores ~1 s wall)
+    lib = load_oracle()
+    # one sample buffer (config-2 bytes of blocks 32.., 4 GiB), hashed over and
+    # over until the measurement has run its share of the CPU work
     nmax = 1 << 17
     buf = np.empty(nmax * bs // 8, dtype=np.uint64)
     lib.oracle_splitmix64_fill(buf.ctypes.data, 32 * bs // 8, buf.size, SEED_C2, 0, 0)
     out = np.empty(nmax * 32, dtype=np.uint8)
 
-    def measure(threads, wall_s):
-        nblk, done, t0 = nmax, 0, time.perf_counter()
-        while True:
-            lib.oracle_hash_chunks(buf.ctypes.data, nblk * bs, bs, out.ctypes.data, threads)
-            done += nblk
-            dt = time.perf_counter() - t0
-            if dt >= wall_s:
-                return done, dt
-
-    res = {}
-    for threads in sorted({4, all_cores}):
-        nblk, dt = measure(threads, target_s * 4.0 / threads if threads > 4 else target_s)
-        res[threads] = (nblk * bs / dt / GIB, nblk)
-    t4 = res[4]
-    return {
-        "value": round(t4[0], 4), "unit": "GiB/s", "cores": 4, "kind": "port",
-        "sample": "%d x %d B config-2 blocks (a 4 GiB sample of blocks 32.. re-hashed; "
-                  "splitmix64 seed 0x5EED0002), oracle/blake2b_oracle.c, 4 threads = "
-                  "reference default --disk-threads" % (t4[1], bs),
-        "all_cores": {"value": round(res[all_cores][0], 4), "cores": all_cores,
-                      "sample_blocks": res[all_cores][1]},
-    }
+    def run(threads):
+        lib.oracle_hash_chunks(buf.ctypes.data, nmax * bs, bs, out.ctypes.data, threads)
+        return nmax * bs
+    return cpu_record(cpu_rates(run, target_s),
+                      "%d x %d B config-2 blocks (4 GiB of blocks 32.., splitmix64 seed "
+                      "0x5EED0002) re-hashed, oracle/blake2b_oracle.c; 4 threads = reference "
+                      "default --disk-threads" % (nmax, bs))
 
 
 def shard(rank, world, nblk_per_gpu):
     """Config 4 range split: rank g owns global blocks [g*n, (g+1)*n)."""
     return rank * nblk_per_gpu, nblk_per_gpu
+
+
+def timed_steps(step, steps, sync, barrier=None):
+    """The timed region of every rank: barrier + sync, exactly `steps` calls
+    of step(i), sync + barrier; returns this rank's wall seconds."""
+    if barrier is not None:
+        barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    sync()
+    if barrier is not None:
+        barrier()
+    return time.perf_counter() - t0
+
+
+def max_over_ranks(seconds, device=None):
+    """The slowest rank's time: all_reduce(MAX) over the process group (a
+    no-op at world size 1).  device: where the reduced tensor lives (the
+    rank's GPU for RCCL, None = host memory for gloo)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([seconds], dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def job_rate(bytes_per_rank_step, world, steps, elapsed_max):
+    """Whole-job GiB/s: all ranks' bytes over the slowest rank's time."""
+    return bytes_per_rank_step * world * steps / elapsed_max / GIB
+
+
+def config4_check(oracle_lib, digests, nbytes, bs, first_block, sample=64):
+    """Config-4 shard parity outside the timed region: the first and last
+    `sample` blocks of this rank's shard (the range boundaries) and `sample`
+    blocks spread over it, regenerated on the host from their global block
+    index and hashed by the oracle.  Returns the number of mismatches."""
+    import numpy as np
+    nblk = nbytes // bs
+    picks = sorted(set(list(range(min(sample, nblk))) +
+                       list(range(max(0, nblk - sample), nblk)) +
+                       [int(x) for x in np.linspace(0, nblk - 1, sample)]))
+    buf = np.empty(bs // 8, dtype=np.uint64)
+    want = np.empty(32, dtype=np.uint8)
+    bad = 0
+    for b in picks:
+        oracle_lib.oracle_splitmix64_fill(buf.ctypes.data, 0, buf.size, SEED_C4, bs // 8,
+                                          first_block + b)
+        oracle_lib.oracle_hash_chunks(buf.ctypes.data, bs, bs, want.ctypes.data, 1)
+        bad += int(digests[32 * b:32 * b + 32].tobytes() != want.tobytes())
+    return bad, len(picks)
 
 
 def config3_layout(total=10 << 30, seed=0x5EED0003):
@@ -181,6 +277,7 @@ def valu_ceiling(ca, nblk, bs, stream, reps=4):
 
 
 def run_config3(args, ca, ctx, dev, stream):
+    import numpy as np
     import torch
     offs, lens, nbytes = config3_layout()
     data = torch.empty(nbytes, dtype=torch.uint8, device=dev)
@@ -203,10 +300,41 @@ def run_config3(args, ca, ctx, dev, stream):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
     hashed = int(lens.astype("int64").sum())
+    got = out.cpu().numpy().reshape(-1, 32)
+    del data, out
+    torch.cuda.empty_cache()
+
+    # oracle check + CPU baseline on the same sample: the first descriptors
+    # whose blocks fill the first 2 GiB of the arena (shuffled order, so all
+    # three classes and the ragged lengths are in it), regenerated on the host
+    lib = load_oracle()
+    k = int(np.searchsorted(offs, 2 << 30))
+    prefix = int(offs[k - 1] + (lens[k - 1] + 127) // 128 * 128)
+    host = np.empty(prefix // 8, dtype=np.uint64)
+    lib.oracle_splitmix64_fill(host.ctypes.data, 0, host.size, 0x5EED0003, 0, 0)
+    s_off = np.ascontiguousarray(offs[:k].astype(np.uint64))
+    s_len = np.ascontiguousarray(lens[:k].astype(np.uint32))
+    want = np.empty((k, 32), dtype=np.uint8)
+    sample_bytes = int(s_len.astype(np.int64).sum())
+
+    def run(threads):
+        lib.oracle_hash_blocks(host.ctypes.data, s_off.ctypes.data, s_len.ctypes.data, k,
+                               want.ctypes.data, threads)
+        return sample_bytes
+    rates = cpu_rates(run, args.cpu_seconds)
+    matches = bool(np.array_equal(got[:k], want))
     return {"metric": "GiB/s block-hashed, config 3 (mixed 4K/32K/1M, 10% ragged, shuffled)",
             "value": round(hashed / dt / GIB, 3), "unit": "GiB/s", "ms_per_step": round(dt * 1e3, 3),
-            "steps": args.steps, "blocks": n, "bytes": hashed,
-            "note": "includes the on-device longest-chain-first sort (order.hip)"}
+            "steps": args.steps, "warmup": args.warmup, "blocks": n, "bytes": hashed,
+            "config": {"workload": "config3: 10 GiB of 4 KiB / 32 KiB / 1 MiB blocks (equal bytes "
+                                   "per class), 10 % ragged, shuffled, device-resident"},
+            "matches_oracle": matches, "oracle_checked_blocks": k,
+            "cpu_baseline": cpu_record(rates, "the first %d descriptors of the config-3 order "
+                                       "(%.2f GiB, all classes, ragged included), "
+                                       "oracle_hash_blocks; 4 threads = reference default "
+                                       "--disk-threads" % (k, sample_bytes / GIB)),
+            "note": "includes the on-device longest-chain-first sort (order.hip); the test "
+                    "suite checks every config-3 digest (test_gpu_fullsize.py)"}
 
 
 def run_config2host(args, ca, ctx, dev, stream):
@@ -306,23 +434,59 @@ def run_config5(args, ca, ctx):
     threads = int(os.environ.get("CIR_SCAN_THREADS", "16"))
     cfg = ca.ScannerConfig.new().threads(threads).add_dir(args.tree_dir, "/")
     times = []
+    index = None
     for i in range(max(1, args.steps)):
         t0 = time.perf_counter()
-        index = ca.v1.scan(cfg, context=ctx)
+        got = ca.v1.scan(cfg, context=ctx)
         times.append(time.perf_counter() - t0)
+        if index is not None and got != index:
+            raise SystemExit("config5: two scans of the same tree differ")
+        index = got
     best = min(times)
+    # checker: the whole tree indexed again by the CPU restatement (every
+    # block digest, the emitter, the footer) on all cores of the GPU's share;
+    # its time is the all-cores leg of the CPU baseline on the full workload
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cpu_indexer
+    lib = cpu_indexer.load()
+    t0 = time.perf_counter()
+    want = cpu_indexer.index(args.tree_dir, 32768, all_cores(), lib)
+    full_s = time.perf_counter() - t0
+    # 4 threads (the reference default) on a bounded sample: directories
+    # d00..d03 (a tenth of the files), indexed as their own trees
+    sample = [os.path.join(args.tree_dir, "d%02d" % i) for i in range(4)]
+    sample = [d for d in sample if os.path.isdir(d)]
+    sample_bytes = sum(os.path.getsize(os.path.join(d, f)) for d in sample for f in os.listdir(d))
+
+    def run(th):
+        for d in sample:
+            cpu_indexer.index(d, 32768, th, lib)
+        return sample_bytes
+    rates = cpu_rates(run, args.cpu_seconds)
+    cpu = cpu_record(rates, "the tree's directories d00..d03 (%d files, %.2f GiB) indexed by "
+                     "oracle/cpu_indexer.py (file-level pool, block_size reads, C BLAKE2b); "
+                     "4 threads = reference default --disk-threads" % (
+                         sum(len(os.listdir(d)) for d in sample), sample_bytes / GIB))
+    cpu["full_tree"] = {"seconds": round(full_s, 3), "cores": all_cores(),
+                        "value": round(nbytes / full_s / GIB, 4)}
     return {"metric": "GiB/s end-to-end index of a tmpfs tree (config 5)",
             "value": round(nbytes / best / GIB, 3), "unit": "GiB/s",
             "seconds_best": round(best, 3), "seconds_all": [round(t, 3) for t in times],
+            "config": {"workload": "config5: %d files x 32 MiB in 40 dirs (%.0f GiB) on tmpfs, "
+                                   "cir_scan_v1 (reads -> pinned -> H2D -> hash -> D2H, footer "
+                                   "on the GPU)" % (nfiles, nbytes / GIB)},
             "files": nfiles, "bytes": nbytes, "index_bytes": len(index),
-            "image_id": ca.get_hash(index).hex(), "tree_gen_s": round(gen_s, 1),
-            "reader_threads": threads, "tree": args.tree_dir}
+            "image_id": ca.get_hash(index).hex(), "matches_oracle": index == want,
+            "tree_gen_s": round(gen_s, 1), "reader_threads": threads, "tree": args.tree_dir,
+            "cpu_baseline": cpu}
 
 
 def run_config1(args, ca, ctx):
     """100 files / 10 MiB, 10 subdirectories, through the `ciruela-index sync`
-    CLI (the indexing half of `ciruela sync --append`), plus the oracle
-    (python restatement of v1::scan) timed on the same tree."""
+    CLI (the indexing half of `ciruela sync --append`, one process: HIP
+    start-up included) and through v1::scan in this process (warm), checked
+    against the scan oracle; CPU baseline = the CPU indexer restatement on
+    the same tree."""
     import subprocess
     import numpy as np
     root = "/tmp/ciruela_cfg1_tree"
@@ -335,19 +499,40 @@ def run_config1(args, ca, ctx):
         os.makedirs(d, exist_ok=True)
         with open(os.path.join(d, "file%03d" % i), "wb") as f:
             f.write(rng.integers(0, 256, size=int(sz), dtype=np.uint8).tobytes())
+    total = int(sizes.sum())
     cli = os.path.join(ROOT, "bin", "ciruela-index")
     t0 = time.perf_counter()
     out = subprocess.check_output([cli, "sync", "--append", root + ":/bench"])
     cli_s = time.perf_counter() - t0
+    cfg = ca.ScannerConfig.new().add_dir(root, "/")  # threads(4), the reference default
+    warm = []
+    for _ in range(max(3, args.steps)):
+        t0 = time.perf_counter()
+        index = ca.v1.scan(cfg, context=ctx)
+        warm.append(time.perf_counter() - t0)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cpu_indexer
     import dirsig_oracle
     t0 = time.perf_counter()
     want = dirsig_oracle.scan(root)
     oracle_s = time.perf_counter() - t0
+    lib = cpu_indexer.load()
+    rates = cpu_rates(lambda th: (cpu_indexer.index(root, 32768, th, lib), total)[1],
+                      args.cpu_seconds)
     image_id = out.decode().split()[0]
+    best = min(warm)
     return {"metric": "config 1: 100-file / 10 MiB tree via `ciruela-index sync --append`",
+            "value": round(total / best / GIB, 4), "unit": "GiB/s",
+            "seconds_best": round(best, 5), "seconds_all": [round(t, 5) for t in warm],
+            "config": {"workload": "config1: 100 files, %d bytes, 10 subdirectories" % total},
             "cli_seconds": round(cli_s, 3), "oracle_python_seconds": round(oracle_s, 3),
-            "image_id": image_id, "matches_oracle": want.endswith(image_id.encode() + b"\n")}
+            "image_id": image_id,
+            "matches_oracle": want.endswith(image_id.encode() + b"\n") and index == want,
+            "cpu_baseline": cpu_record(rates, "the whole config-1 tree indexed by "
+                                       "oracle/cpu_indexer.py (file-level pool, C BLAKE2b), "
+                                       "repeated; 4 threads = reference default --disk-threads"),
+            "note": "value = in-process v1::scan (warm context, threads 4); cli_seconds is one "
+                    "`ciruela-index sync` process including HIP start-up"}
 
 
 def main():
@@ -362,8 +547,15 @@ def main():
 
     import ciruela_amd as ca
 
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one rank per GPU; more ranks than GPUs (a rehearsal of the N>1 path on a
+    # small box, gloo only: RCCL refuses two ranks on one GPU) share them
+    ndev = max(1, torch.cuda.device_count())
+    ranks_per_gpu = (world + ndev - 1) // ndev if world > ndev else 1
+    if ranks_per_gpu > 1:
+        log("warning: %d ranks on %d GPU(s): ranks share GPUs (rehearsal, not a scaling run)"
+            % (world, ndev))
+    torch.cuda.set_device(local % ndev)
+    dev = torch.device("cuda", local % ndev)
     distributed = world > 1 or args.force_dist
     if distributed:
         # RCCL prints its version banner on stdout when the communicator
@@ -373,7 +565,10 @@ def main():
         saved = os.dup(1)
         os.dup2(2, 1)
         try:
-            dist.init_process_group("nccl", device_id=dev)
+            if args.dist_backend == "nccl":
+                dist.init_process_group("nccl", device_id=dev)
+            else:
+                dist.init_process_group("gloo")
             dist.barrier()
         finally:
             sys.stdout.flush()
@@ -384,7 +579,7 @@ def main():
     nblk = args.blocks
     nbytes = nblk * bs
     stream = torch.cuda.current_stream().cuda_stream
-    ctx = ca.Context(device_mask=1 << local, staging_bytes=args.staging_mib << 20)
+    ctx = ca.Context(device_mask=1 << (local % ndev), staging_bytes=args.staging_mib << 20)
 
     if args.workload != "auto":
         if world != 1:
@@ -428,24 +623,15 @@ def main():
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
+
+    def timed_step(i):
         ev[i][0].record()
         step()
         ev[i][1].record()
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed_steps(timed_step, args.steps, torch.cuda.synchronize,
+                          dist.barrier if distributed else None)
     kern_ms = [a.elapsed_time(b) for a, b in ev]
-
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if distributed:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed_max = float(t.item())
+    elapsed_max = max_over_ranks(elapsed, dev if args.dist_backend == "nccl" else None)
 
     # parity spot checks (no oracle here: golden digests + step-to-step identity)
     parity = "ok"
@@ -459,6 +645,14 @@ def main():
             if any(d[i].tobytes().hex() != gold["zero_block"] for i in range(16)) or \
                any(d[i].tobytes().hex() != gold["range_block"] for i in range(16, 32)):
                 parity = "FAIL: golden config-2 blocks differ"
+    c4_checked = None
+    if workload == "config4":
+        import numpy as np
+        oracle_lib = load_oracle()
+        nbad, c4_checked = config4_check(oracle_lib, out.cpu().numpy(), nbytes, bs, first)
+        if nbad:
+            parity = "FAIL: %d of %d sampled config-4 digests differ from the oracle" % (
+                nbad, c4_checked)
     if parity != "ok":
         log("PARITY " + parity)
     valu_ms = valu_ceiling(ca, nblk, bs, stream)
@@ -471,10 +665,9 @@ def main():
         # traffic depends on the launch shape, not on the bytes' values
         cfg_key = "bs%d/n%d/%s" % (bs, nblk, loader_name)
         traffic = load_traffic(cfg_key)
-        total_bytes = nbytes * world * args.steps
         rec = {
             "metric": METRIC,
-            "value": round(total_bytes / elapsed_max / GIB, 3),
+            "value": round(job_rate(nbytes, world, args.steps, elapsed_max), 3),
             "unit": "GiB/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -506,6 +699,10 @@ def main():
             },
             "parity": parity,
         }
+        if c4_checked:
+            rec["parity_checked_blocks"] = c4_checked
+        if ranks_per_gpu > 1:
+            rec["config"]["ranks_per_gpu"] = ranks_per_gpu
         if not distributed and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(bs, args.cpu_seconds)
         print(json.dumps(rec), flush=True)

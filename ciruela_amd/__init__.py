@@ -518,13 +518,12 @@ class ThreadedBlockReader:
         del keep
 
     def register_memory_blocks(self, hash_type, block_size, data, context=None):
-        if hash_type.code != _n.CIR_HASH_BLAKE2B_256:
-            # BlockHash (src/block_id.rs:37-43) is BLAKE2b-256 only
-            raise CiruelaError(_n.CIR_EUNSUPPORTED, "block ids are blake2b/256")
+        """src/blocks.rs:187-204: block ids are Hashes::hash_file(hash_type, ..)
+        digests (put-file passes the index's hash type, put_file/network.rs:56)."""
         ctx = context or default_context()
         ptr, keep = _buf(bytes(data)) if len(data) else (None, None)
-        _n.check(_n.lib.cir_blocks_register_memory(ctx.handle, self._h, ptr, len(data),
-                                                   block_size))
+        _n.check(_n.lib.cir_blocks_register_memory_ht(ctx.handle, self._h, hash_type.code, ptr,
+                                                      len(data), block_size))
         del keep
 
     def read_block(self, block_hash, hint=None):

@@ -83,6 +83,8 @@ _SIGS = {
     "cir_blocks_register_dir": (ctypes.c_int, [c_vp, ctypes.c_char_p, c_vp, ctypes.c_size_t]),
     "cir_blocks_register_memory": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_size_t,
                                                   ctypes.c_uint64]),
+    "cir_blocks_register_memory_ht": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, c_vp,
+                                                     ctypes.c_size_t, ctypes.c_uint64]),
     "cir_blocks_read": (ctypes.c_int, [c_vp, c_vp, ctypes.POINTER(c_vp), c_sizep]),
     "cir_sha512_256": (ctypes.c_int, [c_vp, ctypes.c_size_t, c_vp]),
     "cir_hash_blocks_dev_ht": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, c_vp, c_vp, ctypes.c_size_t,

@@ -380,6 +380,46 @@ __device__ __forceinline__ void hash_chain(const uint8_t* p, uint64_t len, uint6
   }
 }
 
+// The first rem (0..128) bytes of a 16-byte aligned line, zero padded, with
+// 16-byte vector loads: a vector that starts below rem is read whole (it
+// lies inside one 16-byte aligned span, so inside the page that holds the
+// chain's last byte) and the bytes at and past rem are masked off.
+__device__ __forceinline__ void load_line_tail16(uint64_t m[16], const uint8_t* p, uint32_t rem) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    uint4 x = make_uint4(0, 0, 0, 0);
+    if (16u * k < rem) x = q[k];
+    uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int keep = (int)rem - (16 * k + 4 * j);  // bytes of word j below rem
+      w[j] = keep >= 4 ? w[j] : keep <= 0 ? 0u : w[j] & ((1u << (8 * keep)) - 1u);
+    }
+    m[2 * k] = mk64(w[0], w[1]);
+    m[2 * k + 1] = mk64(w[2], w[3]);
+  }
+}
+
+// hash_chain for a 16-byte aligned chain start: every line by 16-byte vector
+// loads (the short last one masked by load_line_tail16), no byte loads.
+__device__ __forceinline__ void hash_chain_al16(const uint8_t* p, uint64_t len, uint64_t h[8]) {
+  init_state(h);
+  const uint32_t nfull = (uint32_t)(len >> 7);
+  const uint32_t rem = (uint32_t)(len & 127u);
+  const uint32_t total = nfull + ((rem != 0u || len == 0) ? 1u : 0u);
+  uint64_t m[16];
+  for (uint32_t i = 0; i < total; ++i) {
+    // one loader for every line (n = 128 reads the whole line); n is opaque
+    // so the per-word masks stay in the loop instead of SGPR-mask hoisting
+    uint32_t n = i < nfull ? 128u : rem;
+    asm volatile("" : "+v"(n));
+    load_line_tail16(m, p + ((uint64_t)i << 7), n);
+    const bool last = i + 1 == total;
+    compress(h, m, last ? len : (uint64_t)(i + 1) << 7, last);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Quad-per-chain mode for long chains (>= kQuadMinLines lines).  A BLAKE2b
 // round is 4 independent G on the columns, then 4 on the diagonals; lane i of

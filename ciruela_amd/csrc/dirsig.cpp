@@ -154,6 +154,29 @@ static bool parse_u64(const std::string& s, uint64_t* v) {
   return true;
 }
 
+// fill_dirs (src/cluster/download.rs:108-167) accepts only RootDir and
+// Normal components in a directory line and needs a file_name() for every
+// entry: "..", "." and empty names are IndexParseEnum::InvalidPath there.
+// Rejecting them here also keeps register_dir (base + path) inside the
+// registered directory.
+static bool valid_name(const std::string& n) {
+  return !n.empty() && n != "." && n != ".." && n.find('/') == std::string::npos &&
+         n.find('\0') == std::string::npos;
+}
+
+static bool valid_dir_path(const std::string& p) {
+  if (p.empty() || p[0] != '/' || p.find('\0') != std::string::npos) return false;
+  size_t i = 1;
+  while (i < p.size()) {
+    size_t j = p.find('/', i);
+    if (j == std::string::npos) j = p.size();
+    const std::string c = p.substr(i, j - i);
+    if (c == "." || c == "..") return false;
+    i = j + 1;
+  }
+  return true;
+}
+
 bool parse(const uint8_t* data, size_t len, Index* out, std::string* err) {
   out->entries.clear();
   std::vector<std::string> lines;
@@ -201,6 +224,10 @@ bool parse(const uint8_t* data, size_t len, Index* out, std::string* err) {
         *err = "bad escape in directory line";
         return false;
       }
+      if (!valid_dir_path(cur_dir)) {
+        *err = "Invalid path in index: " + l;
+        return false;
+      }
       have_dir = true;
       Entry e;
       e.kind = EntryKind::kDir;
@@ -221,6 +248,10 @@ bool parse(const uint8_t* data, size_t len, Index* out, std::string* err) {
     std::string name;
     if (!unescape(tok[0], &name)) {
       *err = "bad escape in entry name";
+      return false;
+    }
+    if (!valid_name(name)) {
+      *err = "Invalid path in index: entry " + tok[0] + " on line " + std::to_string(li + 1);
       return false;
     }
     e.path = cur_dir == "/" ? "/" + name : cur_dir + "/" + name;

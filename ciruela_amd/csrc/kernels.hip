@@ -52,12 +52,19 @@ __global__ __launch_bounds__(kThreads, 5) void k_uniform_glds(const uint8_t* __r
 
 // Hashes::hash_file over one device-resident file, fused in one launch:
 // workgroups [0, ngen_wg) hash the blocks nuni .. nblk-1 (the ragged rest:
-// fewer than 256 whole blocks plus the short last block) with the general
-// loader, the others hash blocks [0, nuni) 64 per wave through LDS.  The
+// fewer than 256 whole blocks plus the short last block) one lane per chain
+// with vector loads (hash_chain_al16: the file is 16-B aligned and bs % 128
+// == 0 whenever this kernel runs; misaligned files go to k_general), the
+// others hash blocks [0, nuni) 64 per wave through LDS.  The
 // ragged workgroups come first so their chains start with the rest instead
 // of trailing the launch.
+// 4 waves per SIMD (128-VGPR budget): the uniform body needs 90 VGPRs, the
+// fused ragged branch ~100; at 5 (96 VGPRs) the ragged branch spilled 6
+// VGPRs to scratch.  4 and 5 waves run config 2 within 0.02 % of each other
+// (profiles/r01/ablib_nt_occ.log: 14.859 vs 14.857 ms): the body is
+// issue-bound, not latency-bound.
 #ifndef CIR_UNI_OCC
-#define CIR_UNI_OCC 5
+#define CIR_UNI_OCC 4
 #endif
 __global__ __launch_bounds__(kThreads, CIR_UNI_OCC) void k_chunks(const uint8_t* __restrict__ data,
                                                          uint64_t nbytes, uint64_t bs,
@@ -70,7 +77,7 @@ __global__ __launch_bounds__(kThreads, CIR_UNI_OCC) void k_chunks(const uint8_t*
     if (b >= nblk) return;
     const uint64_t o = b * bs, rest = nbytes - o;
     uint64_t h[8];
-    hash_chain(data + o, rest < bs ? rest : bs, h);
+    hash_chain_al16(data + o, rest < bs ? rest : bs, h);  // launched only 16-B aligned
     store_digest(out + b * 32u, h);
     return;
   }
@@ -364,6 +371,52 @@ hipError_t launch_chain_step(uint64_t* st, const uint8_t* data, uint32_t n, bool
   return hipGetLastError();
 }
 
+// BlockHash::hash_bytes of one host buffer in one launch (the low-latency
+// single-block path, src/block_id.rs:37-43 as called per received block at
+// src/daemon/tracking/fetch_blocks.rs:77): the workgroup pulls the pinned,
+// device-mapped host bytes over PCIe into device scratch (16-B vectors, four
+// loads in flight per lane), then one quad hashes the chain from there
+// (L2-resident, prefetched one line ahead) and writes the 32-byte digest
+// straight into device-mapped host memory.  No staging copies, no ordering
+// kernel, no D2H copy: one launch per call.
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_single(
+    const uint8_t* __restrict__ src, uint32_t n, uint8_t* __restrict__ scratch,
+    uint8_t* __restrict__ dout) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[128];
+  const uint32_t nv = (n + 15u) >> 4;  // 16-B vectors (src/scratch hold whole vectors)
+  const uint4* s4 = reinterpret_cast<const uint4*>(src);
+  uint4* d4 = reinterpret_cast<uint4*>(scratch);
+  for (uint32_t v = threadIdx.x; v < nv; v += 4u * kThreads) {
+    uint4 r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t j = v + (uint32_t)k * kThreads;
+      if (j < nv) r[k] = s4[j];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t j = v + (uint32_t)k * kThreads;
+      if (j < nv) d4[j] = r[k];
+    }
+  }
+  __threadfence_block();
+  __syncthreads();
+  const uint32_t i = threadIdx.x;
+  if (i >= 4) return;
+  uint32_t addr[48];
+  quad_addr(addr, 0u, i);
+  uint64_t h0, h1;
+  quad_init(i, h0, h1);
+  quad_run<true>(h0, h1, 0, scratch, n, true, true, lds, addr, 0u, i);
+  reinterpret_cast<uint64_t*>(dout)[i] = h0;
+}
+
+hipError_t launch_single(const uint8_t* h_src, uint32_t n, uint8_t* d_scratch, uint8_t* h_out,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(k_single, dim3(1), dim3(kThreads), 0, s, h_src, n, d_scratch, h_out);
+  return hipGetLastError();
+}
+
 // SHA-512/256 over a descriptor batch, one lane per block (dir-signature's
 // HashType::sha512_256()).
 __global__ __launch_bounds__(kThreads, 3) void k_sha_desc(const uint8_t* __restrict__ arena,
@@ -490,7 +543,9 @@ hipError_t launch_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint
   }
   const bool uni_ok = bs % 128u == 0 && (reinterpret_cast<uintptr_t>(data) & 15u) == 0 &&
                       bs / 128u <= 0xffffffffull && bs <= 0xffffffffull / 8u;
-  const uint64_t nuni = uni_ok ? (nbytes / bs) / kThreads * kThreads : 0;
+  if (!uni_ok)  // misaligned base or bs % 128 != 0: every block ragged
+    return launch_general_chunks(data, nbytes, bs, 0, nblk, out, s);
+  const uint64_t nuni = (nbytes / bs) / kThreads * kThreads;
   const uint64_t ngen_wg = grid_for(nblk - nuni, kThreads);
   const uint64_t grid = ngen_wg + nuni / kThreads;
   if (grid > 0x7fffffffull) return hipErrorInvalidValue;

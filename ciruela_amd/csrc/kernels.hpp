@@ -87,6 +87,13 @@ hipError_t launch_sha_desc(const uint8_t* arena, const uint64_t* off, const uint
 hipError_t launch_chain_step(uint64_t* st, const uint8_t* data, uint32_t n, bool final,
                              hipStream_t s);
 
+// One BLAKE2b-256 chain over n bytes of device-mapped pinned host memory
+// h_src (16-B aligned, readable up to n rounded up to 16), staged through
+// d_scratch (same rounding) by the kernel itself; the digest is written to
+// device-mapped host memory h_out (32 B).  One launch, nothing else.
+hipError_t launch_single(const uint8_t* h_src, uint32_t n, uint8_t* d_scratch, uint8_t* h_out,
+                         hipStream_t s);
+
 // Compare n digests (32 B each, both 16-B aligned) with the expected ones:
 // ok[b] = 1 / 0 (ok may be null); *nbad += mismatches (nbad may be null).
 hipError_t launch_verify(const uint8_t* got, const uint8_t* want, uint64_t n, uint8_t* ok,

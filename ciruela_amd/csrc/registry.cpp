@@ -144,12 +144,16 @@ int cir_blocks_register_dir(cir_blocks* h, const char* dir, const uint8_t* index
 // size = min(len, (idx+1)*bs), an end offset used as a length (:201), so its
 // reads of blocks 1.. over-read or panic.  Here block idx covers exactly the
 // bytes its hash was computed over: [idx*bs, min(len, (idx+1)*bs)).
-int cir_blocks_register_memory(cir_ctx* ctx, cir_blocks* h, const uint8_t* data, size_t len,
-                               uint64_t block_size) {
+// The hash type is the index's (put-file passes it through,
+// src/client/put_file/network.rs:56): every block id is
+// Hashes::hash_file(hash_type, ..)'s digest of the block.
+int cir_blocks_register_memory_ht(cir_ctx* ctx, cir_blocks* h, int hash_type, const uint8_t* data,
+                                  size_t len, uint64_t block_size) {
   if (!ctx || !h || (len && !data)) return fail(CIR_EINVAL, "null pointer");
+  if (!valid_hash_type(hash_type)) return fail(CIR_EINVAL, "unknown hash type");
   uint8_t* hashes = nullptr;
   size_t n = 0;
-  int rc = cir_hash_memory(ctx, data, len, block_size, &hashes, &n);
+  int rc = cir_hash_memory_ht(ctx, hash_type, data, len, block_size, &hashes, &n);
   if (rc) return rc;
   auto buf = std::make_shared<std::vector<uint8_t>>(data, data + len);
   auto* m = reinterpret_cast<BlockMap*>(h);
@@ -165,6 +169,11 @@ int cir_blocks_register_memory(cir_ctx* ctx, cir_blocks* h, const uint8_t* data,
   }
   free(hashes);
   return CIR_OK;
+}
+
+int cir_blocks_register_memory(cir_ctx* ctx, cir_blocks* h, const uint8_t* data, size_t len,
+                               uint64_t block_size) {
+  return cir_blocks_register_memory_ht(ctx, h, CIR_HASH_BLAKE2B_256, data, len, block_size);
 }
 
 // GetBlock::read_block (src/blocks.rs:207-240).  Unlike the reference's

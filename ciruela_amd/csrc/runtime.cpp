@@ -29,6 +29,7 @@ int hip_fail(hipError_t e, const char* what) {
 }
 
 Device::~Device() {
+  DeviceGuard guard;
   (void)hipSetDevice(id);
   for (Slot& s : slot) {
     if (s.done) (void)hipEventSynchronize(s.done);
@@ -60,6 +61,11 @@ Device::~Device() {
   if (aux_fork) (void)hipEventDestroy(aux_fork);
   if (aux_join) (void)hipEventDestroy(aux_join);
   if (aux) (void)hipStreamDestroy(aux);
+  if (single) (void)hipStreamSynchronize(single);
+  (void)hipHostFree(single_h);
+  (void)hipHostFree(single_out);
+  (void)hipFree(single_d);
+  if (single) (void)hipStreamDestroy(single);
   if (compute) (void)hipStreamDestroy(compute);
   if (copy) (void)hipStreamDestroy(copy);
 }
@@ -126,17 +132,19 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
   // Every batch is ordered (even a single chain: an index footer is one long
   // chain and runs in quad mode).
   if (n == 0) return CIR_OK;
+  if (n > (uint64_t)INT32_MAX)  // hipCUB's item count is an int (order.hip)
+    return fail(CIR_EINVAL, "more than 2^31-1 descriptors in one ordered batch");
   std::lock_guard<std::mutex> lk(d.order_mu);
+  // Streams, events and the ordering scratch live on d's device, whatever
+  // the caller's current device is; the caller's device is restored on exit.
+  DeviceGuard guard;
+  CIR_HIP(hipSetDevice(d.id));
   const size_t need = dev::order_scratch_bytes(n);
-  if (!d.order_free) {  // created on d's device, whatever the caller's current one is
-    int cur = 0;
-    CIR_HIP(hipGetDevice(&cur));
-    CIR_HIP(hipSetDevice(d.id));
+  if (!d.order_free) {
     CIR_HIP(hipEventCreateWithFlags(&d.order_free, hipEventDisableTiming));
     CIR_HIP(hipStreamCreateWithFlags(&d.aux, hipStreamNonBlocking));
     CIR_HIP(hipEventCreateWithFlags(&d.aux_fork, hipEventDisableTiming));
     CIR_HIP(hipEventCreateWithFlags(&d.aux_join, hipEventDisableTiming));
-    CIR_HIP(hipSetDevice(cur));
   }
   if (need > d.order_cap) {
     CIR_HIP(hipEventSynchronize(d.order_free));
@@ -264,6 +272,7 @@ static void parallel_items(size_t n, uint64_t bytes, const std::function<void(si
 static int run_blocks(cir_ctx* ctx, Device& d, const uint8_t* arena, const uint64_t* off,
                       const uint32_t* len, size_t b0, size_t b1, uint8_t* out, int ht) {
   std::lock_guard<std::mutex> lk(d.mu);
+  DeviceGuard guard;
   CIR_HIP(hipSetDevice(d.id));
   const uint64_t cap = ctx->staging;
   const uint64_t cap_blk = std::max<uint64_t>(cap / 512, 4096);
@@ -343,6 +352,7 @@ using Reader = std::function<int64_t(uint8_t*, uint64_t)>;
 static int run_file_dev(cir_ctx* ctx, Device& d, const Reader& rd, uint64_t bs,
                         uint64_t* size_out, std::vector<uint8_t>& hashes, int ht) {
   std::lock_guard<std::mutex> lk(d.mu);
+  DeviceGuard guard;
   CIR_HIP(hipSetDevice(d.id));
   uint64_t chunk = ctx->staging / bs * bs;
   if (chunk == 0) chunk = bs;
@@ -493,6 +503,7 @@ int cir_init(cir_ctx** out, uint32_t device_mask, uint64_t staging_bytes) {
   hipError_t e = hipGetDeviceCount(&n);
   if (e != hipSuccess || n == 0)
     return fail(CIR_ENODEV, std::string("no HIP device: ") + hipGetErrorString(e));
+  DeviceGuard guard;
   auto ctx = std::make_unique<cir_ctx>();
   ctx->staging = staging_bytes ? staging_bytes : (256ull << 20);
   for (int i = 0; i < n && i < 32; ++i) {
@@ -576,7 +587,9 @@ int cir_hash_blocks_dev_ht(cir_ctx* ctx, int hash_type, const void* d_arena,
     return fail(CIR_EINVAL, "null device pointer");
   if (reinterpret_cast<uintptr_t>(d_out) & 15u)
     return fail(CIR_EINVAL, "d_out must be 16-byte aligned");
-  if (nblk > 0xffffffffull) return fail(CIR_EINVAL, "more than 2^32 descriptors");
+  // descriptor indices are 32-bit in the kernels and the ordering sorts an
+  // int-sized item count (hipCUB): one call takes at most 2^31-1 blocks
+  if (nblk > (size_t)INT32_MAX) return fail(CIR_EINVAL, "more than 2^31-1 descriptors");
   hipStream_t s = (hipStream_t)stream;
   // Context-less calls hash in descriptor order, one lane per chain; with a
   // context the batch is ordered longest chain first on the device
@@ -635,12 +648,53 @@ int cir_hash_blocks(cir_ctx* ctx, const uint8_t* h_arena, const uint64_t* off,
   return cir_hash_blocks_ht(ctx, CIR_HASH_BLAKE2B_256, h_arena, off, len, nblk, h_out);
 }
 
+// Inputs up to this size take the one-launch path (k_single): the chain of
+// a larger input runs for milliseconds, so the staged path's fixed cost no
+// longer matters there.
+constexpr size_t kSingleMax = 16ull << 20;
+
+// BlockHash::hash_bytes in one kernel launch: copy into a pinned buffer the
+// GPU reads over PCIe, launch, wait, read the digest the kernel wrote into
+// mapped host memory.
+static int single_launch(Device& d, const uint8_t* p, size_t n, uint8_t* out) {
+  std::lock_guard<std::mutex> lk(d.single_mu);
+  DeviceGuard guard;
+  CIR_HIP(hipSetDevice(d.id));
+  if (!d.single) {
+    CIR_HIP(hipStreamCreateWithFlags(&d.single, hipStreamNonBlocking));
+    CIR_HIP(hipHostMalloc(&d.single_out, 64, hipHostMallocMapped | hipHostMallocCoherent));
+  }
+  const size_t need = (n + 15) & ~(size_t)15;
+  if (need > d.single_cap) {
+    (void)hipHostFree(d.single_h);
+    (void)hipFree(d.single_d);
+    d.single_h = nullptr;
+    d.single_d = nullptr;
+    d.single_cap = 0;
+    const size_t cap = std::max<size_t>(need, 64u << 10);
+    CIR_HIP(hipHostMalloc(&d.single_h, cap, hipHostMallocMapped | hipHostMallocCoherent));
+    CIR_HIP(hipMalloc(&d.single_d, cap));
+    d.single_cap = cap;
+  }
+  if (n) memcpy(d.single_h, p, n);
+  uint8_t* h_src = nullptr;
+  uint8_t* h_dst = nullptr;
+  CIR_HIP(hipHostGetDevicePointer((void**)&h_src, d.single_h, 0));
+  CIR_HIP(hipHostGetDevicePointer((void**)&h_dst, d.single_out, 0));
+  CIR_HIP(dev::launch_single(h_src, (uint32_t)n, d.single_d, h_dst, d.single));
+  CIR_HIP(hipStreamSynchronize(d.single));
+  memcpy(out, d.single_out, 32);
+  return CIR_OK;
+}
+
 static int single_shot(int ht, const uint8_t* p, size_t n, uint8_t* out) {
   if (!out || (n && !p)) return fail(CIR_EINVAL, "null pointer");
   if (n > 0xffffffffull) return fail(CIR_EINVAL, "block longer than 4 GiB");
   cir_ctx* ctx = nullptr;
   int rc = default_ctx(&ctx);
   if (rc) return rc;
+  if (ht == CIR_HASH_BLAKE2B_256 && n <= kSingleMax && !std::getenv("CIR_SINGLE_STAGED"))
+    return single_launch(*ctx->devs[0], p, n, out);
   static const uint8_t empty = 0;
   const uint64_t off = 0;
   const uint32_t len = (uint32_t)n;

@@ -25,6 +25,25 @@ int hip_fail(hipError_t e, const char* what);
     if (cir_e_ != hipSuccess) return hip_fail(cir_e_, #expr); \
   } while (0)
 
+// Restores the calling thread's current HIP device on scope exit.  Every
+// public entry point that switches device holds one, so a caller working on
+// GPU k finds GPU k current again after any cir_* call (the header's NULL
+// stream means "the current device's null stream").
+class DeviceGuard {
+ public:
+  DeviceGuard() {
+    if (hipGetDevice(&prev_) != hipSuccess) prev_ = -1;
+  }
+  ~DeviceGuard() {
+    if (prev_ >= 0) (void)hipSetDevice(prev_);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+
+ private:
+  int prev_ = -1;
+};
+
 // One staging slot: a pinned host buffer and its device twin, plus the
 // descriptor and digest buffers of the blocks packed into it.
 struct Slot {
@@ -74,6 +93,14 @@ struct Device {
   uint8_t* chain_d[2] = {nullptr, nullptr};
   size_t chain_cap[2] = {0, 0};
   hipEvent_t chain_done[2] = {nullptr, nullptr};
+  // low-latency single-block hash (cir_blake2b256): own stream, a pinned
+  // device-mapped input buffer, device scratch and a mapped digest slot
+  std::mutex single_mu;
+  hipStream_t single = nullptr;
+  uint8_t* single_h = nullptr;
+  uint8_t* single_d = nullptr;
+  uint8_t* single_out = nullptr;
+  size_t single_cap = 0;
   ~Device();
   int ensure_slot(Slot& s, uint64_t bytes, uint64_t nblk);
 };

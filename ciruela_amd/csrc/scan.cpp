@@ -183,6 +183,7 @@ static int hash_range(cir_ctx* ctx, Device& d, const std::vector<ScanFile>& file
                       unsigned threads, int ht, std::vector<uint8_t>& digests, uint64_t b0,
                       uint64_t b1, const std::function<int(uint64_t)>& done) {
   std::lock_guard<std::mutex> lk(d.mu);
+  DeviceGuard guard;
   CIR_HIP(hipSetDevice(d.id));
   const uint64_t cap = std::max<uint64_t>(ctx->staging, bs + 16);
   const uint64_t cap_blk = std::max<uint64_t>(cap / 512, 4096);
@@ -485,6 +486,7 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
   dirsig::Emitter em(hdr);
   Device& dv = *ctx->devs[0];
   std::lock_guard<std::mutex> chain_lock(dv.chain_mu);
+  DeviceGuard guard;  // the caller's current device is restored on return
   CIR_HIP(hipSetDevice(dv.id));
   FooterChain chain(dv);
   int rc = incremental ? chain.start() : CIR_OK;
@@ -546,10 +548,13 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
 // RawIndex::into_mut + MutableIndex::to_raw_data: parse, rebuild the tree and
 // re-emit it in the reference's order with a freshly computed footer.
 int cir_index_rewrite(cir_ctx* ctx, const uint8_t* in, size_t len, uint8_t** out, size_t* out_len) {
-  if (!ctx || !in || !out || !out_len) return fail(CIR_EINVAL, "null pointer");
+  if (!in || !out || !out_len) return fail(CIR_EINVAL, "null pointer");
   dirsig::Index idx;
   std::string err;
+  // parsed before the context is needed: a malformed index is a ParseError
+  // whatever the device state (RawIndex::into_mut, src/cluster/download.rs:175-181)
   if (!dirsig::parse(in, len, &idx, &err)) return fail(CIR_EPARSE, "ParseError: " + err);
+  if (!ctx) return fail(CIR_EINVAL, "null ctx");
   Tree root;
   Tree* cur = &root;
   std::vector<std::string> parts;

@@ -18,6 +18,8 @@
  *   - `stream` arguments are hipStream_t passed as void* (NULL = the null
  *     stream of the calling thread's current device).  *_dev calls are
  *     asynchronous on that stream and never synchronise the device.
+ *   - no call changes the calling thread's current HIP device: entry points
+ *     that work on other devices restore it before returning.
  *   - buffers returned through `uint8_t**` are released with cir_free().
  */
 #ifndef CIRUELA_BLOCKHASH_H
@@ -43,7 +45,7 @@ enum cir_status {
   CIR_ENOTFOUND = -6,  /* ReadError::NotFound (src/index.rs:78, src/blocks.rs:101) */
   CIR_EHASHSIZE = -7,  /* DirError::HashSize (src/blocks.rs:123) */
   CIR_ENODEV = -8,     /* no usable gfx950 device */
-  CIR_EUNSUPPORTED = -9 /* hash type not implemented on the GPU yet */
+  CIR_EUNSUPPORTED = -9 /* reserved (every dir-signature hash type is implemented) */
 };
 
 /* dir-signature HashType (external crate 0.2.9; header tokens in the index) */
@@ -190,9 +192,14 @@ void cir_blocks_free(cir_blocks* h);
 size_t cir_blocks_len(cir_blocks* h);
 /* register_dir (src/blocks.rs:145-183): CIR_EPARSE / CIR_EHASHSIZE. */
 int cir_blocks_register_dir(cir_blocks* h, const char* dir, const uint8_t* index, size_t len);
-/* register_memory_blocks (src/blocks.rs:187-204), hashed on the GPU. */
+/* register_memory_blocks(HashType::blake2b_256(), ..) (src/blocks.rs:187-204),
+ * hashed on the GPU. */
 int cir_blocks_register_memory(cir_ctx* ctx, cir_blocks* h, const uint8_t* data, size_t len,
                                uint64_t block_size);
+/* register_memory_blocks(hash_type, block_size, data) with the index's own
+ * hash type (put-file, src/client/put_file/network.rs:56). */
+int cir_blocks_register_memory_ht(cir_ctx* ctx, cir_blocks* h, int hash_type, const uint8_t* data,
+                                  size_t len, uint64_t block_size);
 /* GetBlock::read_block (src/blocks.rs:207-240); CIR_ENOTFOUND if absent. */
 int cir_blocks_read(cir_blocks* h, const uint8_t hash[CIR_DIGEST_BYTES], uint8_t** data_out,
                     size_t* len_out);

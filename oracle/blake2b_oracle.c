@@ -200,6 +200,95 @@ int oracle_hash_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint8_
   return run(&j, threads);
 }
 
+/* ---- the reference CPU indexer's hashing loop, restated: v1::scan hashes
+ * whole files on a pool of `threads` CPU workers (ScannerConfig::threads,
+ * src/client/sync/uploads.rs:50-53; default 4, src/client/global_options.rs:13),
+ * each worker reading its file in block_size chunks and hashing every chunk
+ * (Hashes::hash_file).  File i's digests go to out + 32 * first[i]; a file
+ * must hold exactly ceil(size / bs) blocks of the size the caller planned
+ * (returned as -EIO otherwise). ---- */
+#include <errno.h>
+#include <fcntl.h>
+#include <unistd.h>
+
+struct files_job {
+  const char* const* paths;
+  const uint64_t* first;
+  const uint64_t* nblk;
+  size_t n, next;
+  uint64_t bs;
+  uint8_t* out;
+  int err;
+  pthread_mutex_t mu;
+};
+
+static void* files_worker(void* arg) {
+  struct files_job* j = (struct files_job*)arg;
+  uint8_t* buf = (uint8_t*)malloc(j->bs ? j->bs : 1);
+  if (!buf) return NULL;
+  for (;;) {
+    pthread_mutex_lock(&j->mu);
+    size_t f = j->next++;
+    int stop = j->err != 0;
+    pthread_mutex_unlock(&j->mu);
+    if (f >= j->n || stop) break;
+    int fd = open(j->paths[f], O_RDONLY);
+    int e = fd < 0 ? errno : 0;
+    uint64_t b = 0;
+    while (!e) {
+      uint64_t got = 0;
+      while (got < j->bs) {
+        ssize_t r = read(fd, buf + got, j->bs - got);
+        if (r < 0 && errno == EINTR) continue;
+        if (r < 0) e = errno;
+        if (r <= 0) break;
+        got += (uint64_t)r;
+      }
+      if (e || got == 0) break;
+      if (b >= j->nblk[f]) {
+        e = EIO;
+        break;
+      }
+      oracle_blake2b256(j->out + 32 * (j->first[f] + b), buf, got);
+      ++b;
+      if (got < j->bs) break;
+    }
+    if (fd >= 0) close(fd);
+    if (!e && b != j->nblk[f]) e = EIO;
+    if (e) {
+      pthread_mutex_lock(&j->mu);
+      if (!j->err) j->err = e;
+      pthread_mutex_unlock(&j->mu);
+    }
+  }
+  free(buf);
+  return NULL;
+}
+
+int oracle_hash_files(const char* const* paths, const uint64_t* first, const uint64_t* nblk,
+                      size_t n, uint64_t bs, uint8_t* out, int threads) {
+  if (bs == 0) return -EINVAL;
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  struct files_job j;
+  memset(&j, 0, sizeof j);
+  j.paths = paths;
+  j.first = first;
+  j.nblk = nblk;
+  j.n = n;
+  j.bs = bs;
+  j.out = out;
+  pthread_mutex_init(&j.mu, NULL);
+  pthread_t th[256];
+  int started = 0;
+  for (int i = 1; i < threads; ++i)
+    if (pthread_create(&th[started], NULL, files_worker, &j) == 0) ++started;
+  files_worker(&j);
+  for (int i = 0; i < started; ++i) pthread_join(th[i], NULL);
+  pthread_mutex_destroy(&j.mu);
+  return -j.err;
+}
+
 /* ---- SHA-512/256 (FIPS 180-4), dir-signature's HashType::sha512_256();
  * the reference's index fixture (src/cluster/download.rs:357-366) uses it. */
 static const uint64_t SHA_K[80] = {

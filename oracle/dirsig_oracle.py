@@ -75,11 +75,12 @@ def emit(hash_name, block_size, dirs, keep_empty=False):
     return header + body + footer
 
 
-def scan(root, block_size=32768, hash_name="blake2b/256"):
-    """Index bytes of the tree at `root` (mounted at '/')."""
+def walk(root):
+    """The tree at `root` mounted at '/': [(vpath, [entries])] in emission
+    order, file entries ('f', name, exe, size, real_path) not yet hashed."""
     dirs = []
 
-    def walk(real, vpath):
+    def rec(real, vpath):
         names = sorted(os.listdir(os.fsencode(real)))
         entries, subdirs = [], []
         for n in names:
@@ -88,19 +89,42 @@ def scan(root, block_size=32768, hash_name="blake2b/256"):
             if stat.S_ISDIR(st.st_mode):
                 subdirs.append(n)
             elif stat.S_ISREG(st.st_mode):
-                with open(p, "rb") as f:
-                    data = f.read()
-                entries.append(("f", n, bool(st.st_mode & 0o111), len(data),
-                                block_hashes(data, block_size, hash_name)))
+                entries.append(("f", n, bool(st.st_mode & 0o111), st.st_size, p))
             elif stat.S_ISLNK(st.st_mode):
                 entries.append(("s", n, os.readlink(p)))
         dirs.append((vpath, entries))
         for n in subdirs:
-            walk(os.path.join(os.fsencode(real), n),
-                 (b"/" + n) if vpath == b"/" else vpath + b"/" + n)
+            rec(os.path.join(os.fsencode(real), n),
+                (b"/" + n) if vpath == b"/" else vpath + b"/" + n)
 
-    walk(root, b"/")
-    return emit(hash_name, block_size, dirs, keep_empty=True)
+    rec(root, b"/")
+    return dirs
+
+
+def scan(root, block_size=32768, hash_name="blake2b/256", block_hasher=None, files_hasher=None):
+    """Index bytes of the tree at `root` (mounted at '/').
+
+    block_hasher(data, block_size) -> [digest, ...] replaces block_hashes
+    per file; files_hasher(paths, sizes, block_size) -> [[digest, ...], ...]
+    hashes every file at once (the threaded C restatement of the CPU
+    indexer's file-level pool, oracle/blake2b_oracle.c oracle_hash_files).
+    The footer is always hashlib's."""
+    dirs = walk(root)
+    files = [e for _, entries in dirs for e in entries if e[0] == "f"]
+    if files_hasher is not None:
+        digests = files_hasher([e[4] for e in files], [e[3] for e in files], block_size)
+    else:
+        hasher = block_hasher or (lambda data, bs: block_hashes(data, bs, hash_name))
+        digests = []
+        for e in files:
+            with open(e[4], "rb") as f:
+                data = f.read()
+            assert len(data) == e[3], "file changed during the scan"
+            digests.append(hasher(data, block_size))
+    it = iter(digests)
+    out = [(vpath, [(e[0], e[1], e[2], e[3], next(it)) if e[0] == "f" else e for e in entries])
+           for vpath, entries in dirs]
+    return emit(hash_name, block_size, out, keep_empty=True)
 
 
 def parse(index):

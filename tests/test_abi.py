@@ -142,3 +142,51 @@ def test_cli_usage():
     cli = os.path.join(ROOT, "bin", "ciruela-index")
     p = subprocess.run([cli], capture_output=True)
     assert p.returncode == 2 and b"usage" in p.stderr
+
+
+BAD_PATH_INDEXES = [
+    # fill_dirs accepts only RootDir / Normal components (src/cluster/download.rs:120-145)
+    b"DIRSIGNATURE.v1 blake2b/256 block_size=4096\n/\n/../etc\n  passwd f 0\n",
+    b"DIRSIGNATURE.v1 blake2b/256 block_size=4096\n/\n/a/./b\n  f f 0\n",
+    # an entry needs a file_name() (:148-162)
+    b"DIRSIGNATURE.v1 blake2b/256 block_size=4096\n/\n  .. f 0\n",
+    b"DIRSIGNATURE.v1 blake2b/256 block_size=4096\n/\n  . f 0\n",
+    b"DIRSIGNATURE.v1 blake2b/256 block_size=4096\n/\n  a\\x2fb f 0\n",
+    b"DIRSIGNATURE.v1 blake2b/256 block_size=4096\n/\n  .. s /etc\n",
+]
+
+
+@pytest.mark.parametrize("bad", BAD_PATH_INDEXES)
+def test_invalid_paths_rejected(tmp_path, bad):
+    """IndexParseEnum::InvalidPath: `..`, `.` and names with a slash are
+    rejected by register_dir and by the rewrite (RawIndex::into_mut), so a
+    registered block never maps outside its directory."""
+    import ctypes
+    idx = bad + b"ab" * 32 + b"\n"
+    r = ca.ThreadedBlockReader()
+    with pytest.raises(ca.DirError) as e:
+        r.register_dir(str(tmp_path), idx)
+    assert e.value.status == _native.CIR_EPARSE
+    assert b"Invalid path" in _native.lib.cir_last_error()
+    out, ln = ctypes.c_void_p(), ctypes.c_size_t()
+    rc = _native.lib.cir_index_rewrite(None, idx, len(idx), ctypes.byref(out), ctypes.byref(ln))
+    assert rc == _native.CIR_EPARSE
+    assert len(r) == 0
+
+
+def test_valid_odd_names_still_parse(tmp_path):
+    """Names that merely look like paths stay valid: `...`, `.x`, escaped bytes."""
+    idx = (b"DIRSIGNATURE.v1 blake2b/256 block_size=4096\n/\n  ... f 0\n  .x f 0\n"
+           b"  a\\x20b f 0\n/sub..dir\n  f f 0\n" + b"ab" * 32 + b"\n")
+    ca.ThreadedBlockReader().register_dir(str(tmp_path), idx)
+
+
+def test_descriptor_count_limit():
+    """cir_hash_blocks_dev_ht takes at most 2^31-1 descriptors (32-bit block
+    indices in the kernels, an int item count in the hipCUB sort): larger
+    batches are rejected before anything touches a device."""
+    lib = _native.lib
+    for n in (1 << 31, (1 << 32) + 5):
+        rc = lib.cir_hash_blocks_dev_ht(None, _native.CIR_HASH_BLAKE2B_256, 16, 16, 16, n, 32, None)
+        assert rc == _native.CIR_EINVAL
+        assert b"2^31-1" in lib.cir_last_error()

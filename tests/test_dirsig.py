@@ -6,6 +6,7 @@ rule, not the blake2b hash (that is pinned in test_oracle.py).
 """
 import hashlib
 import os
+import random
 
 import dirsig_oracle
 import ciruela_amd as ca
@@ -59,11 +60,31 @@ def test_escape():
 
 
 def test_library_parser_on_fixture(dirsig_example, tmp_path):
-    """The product's parser accepts the fixture (sha512/256 parses; only
-    hashing it is GPU-unsupported) and maps every block (register_dir)."""
+    """The product's parser accepts the fixture (a sha512/256 index) and
+    maps every block (register_dir); re-hashing it on the GPU is covered by
+    the -m gpu tests."""
     idx = dirsig_example["index"].encode()
     assert ca.get_hash(idx) == bytes.fromhex(
         "552ca5730ee95727e890a2155c88609d244624034ff70de264cf88220d11d6df")
     r = ca.ThreadedBlockReader()
     r.register_dir(str(tmp_path), idx)
     assert len(r) == 3
+
+
+def test_cpu_indexer_matches_scan_oracle(tmp_path):
+    """oracle/cpu_indexer.py (the threaded C restatement of the reference CPU
+    indexer: whole files on `threads` workers, block_size chunks) emits the
+    same index as the pure-Python scan oracle, at 1 and 4 threads."""
+    import cpu_indexer
+    rnd = random.Random(7)
+    for i, size in enumerate([0, 1, 127, 128, 129, 4096, 4097, 3 * 4096, 70000]):
+        d = tmp_path / ("d%d" % (i % 3))
+        d.mkdir(exist_ok=True)
+        (d / ("f%d" % i)).write_bytes(bytes(rnd.randrange(256) for _ in range(size)))
+    (tmp_path / "d0" / "exe").write_bytes(b"#!/bin/sh\n")
+    (tmp_path / "d0" / "exe").chmod(0o755)
+    (tmp_path / "empty").mkdir()
+    os.symlink("d0/f0", tmp_path / "link")
+    want = dirsig_oracle.scan(str(tmp_path), 4096)
+    for threads in (1, 4):
+        assert cpu_indexer.index(str(tmp_path), 4096, threads) == want

@@ -142,3 +142,96 @@ def test_quad_file_above_4gib(gpu, oracle):
     oracle.oracle_hash_chunks(host.ctypes.data, nbytes, bs, want.ctypes.data, THREADS)
     bad = np.nonzero((got != want.reshape(-1, 32)).any(axis=1))[0]
     assert bad.size == 0, "blocks %s differ" % bad[:8]
+
+
+SEED_C4 = 0x5EED0004
+
+
+def host_fill_blocks(oracle, buf, word0, seed, block_words, first_block):
+    """buf (uint64) = words word0.. of the per-block splitmix64 streams
+    (block i seeded seed ^ (first_block + i)), filled in parallel."""
+    n = buf.size
+    step = max(1, (n + THREADS - 1) // THREADS)
+
+    def part(k):
+        a, b = k * step, min(n, (k + 1) * step)
+        if a < b:
+            oracle.oracle_splitmix64_fill(buf.ctypes.data + 8 * a, word0 + a, b - a, seed,
+                                          block_words, first_block)
+
+    with ThreadPoolExecutor(THREADS) as ex:
+        list(ex.map(part, range(THREADS)))
+
+
+def test_config4_last_shard_full(gpu, oracle):
+    """Config 4 (BASELINE.json configs[3]): 256 GiB of 32 KiB
+    blocks range-split over 8 GPUs, rank g owning global blocks
+    [g*2^20, (g+1)*2^20), block i filled with splitmix64 seeded
+    0x5EED0004 ^ i -- exactly as bench.py's N>1 path fills HBM
+    (bench.shard + cir_fill_splitmix64_dev).  The last rank's full 32 GiB
+    shard (first block 7 * 2^20) is hashed through cir_hash_chunks_dev and
+    EVERY digest is checked against the threaded oracle, which regenerates
+    each block from its global index alone."""
+    import sys
+    import torch
+    from conftest import ROOT
+    sys.path.insert(0, ROOT)
+    import bench
+    nblk, world, rank = 1 << 20, 8, 7
+    first, count = bench.shard(rank, world, nblk)
+    assert (first, count) == (7 << 20, 1 << 20)
+    nbytes = count * BS
+    data = torch.empty(nbytes, dtype=torch.uint8, device="cuda:0")
+    gpu._n.check(gpu._n.lib.cir_fill_splitmix64_dev(data.data_ptr(), nbytes, SEED_C4, BS, first,
+                                                    0))
+    ctx = gpu.Context(device_mask=1)
+    out = torch.empty(count * 32, dtype=torch.uint8, device="cuda:0")
+    ctx.hash_chunks_dev(data.data_ptr(), nbytes, BS, out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().reshape(count, 32)
+    del data
+    per = 32768  # 1 GiB of host data at a time
+    words = np.empty(per * BS // 8, dtype=np.uint64)
+    want = np.zeros((per, 32), dtype=np.uint8)
+    for b0 in range(0, count, per):
+        host_fill_blocks(oracle, words, b0 * BS // 8, SEED_C4, BS // 8, first)
+        oracle.oracle_hash_chunks(words.ctypes.data, per * BS, BS, want.ctypes.data, THREADS)
+        bad = np.nonzero((got[b0:b0 + per] != want).any(axis=1))[0]
+        assert bad.size == 0, "global blocks %s differ" % (bad[:8] + first + b0)
+    # bench.py's own N>1 parity check agrees (the range boundaries + a spread)
+    nbad, checked = bench.config4_check(bench.load_oracle(), out.cpu().numpy(), nbytes, BS, first)
+    assert nbad == 0 and checked >= 128
+
+
+def test_scan_tree_above_2gib(gpu, oracle, tmp_path):
+    """cir_scan_v1 through the 3-slot staging pipeline on a 2.3 GiB tree (9+
+    full 256 MiB batches, files straddling batches, ragged tails, an empty
+    file, nested dirs), index byte for byte against the CPU indexer
+    restatement (every block digest by the threaded C oracle, emitter and
+    footer by dirsig_oracle)."""
+    import cpu_indexer
+    root = "/dev/shm" if os.path.isdir("/dev/shm") else str(tmp_path)
+    import tempfile
+    import shutil
+    top = tempfile.mkdtemp(prefix="cir_scan2g_", dir=root)
+    try:
+        rng = np.random.default_rng(0x5EED2)
+        sizes = [(40 << 20) + 12345, 0, 1, 32767, 32768, 32769, (300 << 20) - 7]
+        sizes += [int(x) for x in rng.integers(1 << 20, 60 << 20, size=56)]
+        total = 0
+        for i, sz in enumerate(sizes):
+            d = os.path.join(top, "d%d" % (i % 5), "e%d" % (i % 3))
+            os.makedirs(d, exist_ok=True)
+            blob = rng.integers(0, 1 << 63, size=(sz + 7) // 8, dtype=np.uint64).tobytes()[:sz]
+            with open(os.path.join(d, "f%03d.bin" % i), "wb") as f:
+                f.write(blob)
+            total += sz
+        assert total > (2 << 30)
+        ctx = gpu.Context(device_mask=1)  # default 256 MiB staging
+        cfg = gpu.ScannerConfig.new().threads(16).add_dir(top, "/")
+        got = gpu.v1.scan(cfg, context=ctx)
+        want = cpu_indexer.index(top, 32768, THREADS)
+        assert got == want
+        assert gpu.get_hash(got) == bytes.fromhex(want.rstrip(b"\n").split(b"\n")[-1].decode())
+    finally:
+        shutil.rmtree(top, ignore_errors=True)

@@ -737,3 +737,76 @@ def test_randomized_batches_and_files(gpu, ctx, oracle, seed):
     torch.cuda.synchronize()
     fh = fdata.cpu().numpy()[skew:].copy()
     assert first_bad(fout.cpu().numpy(), oracle_chunks(oracle, fh, nbytes, bs)) is None
+
+
+def test_reference_hidden_line_on_gpu(gpu, small_ctx, tmp_path, dirsig_example):
+    """The one block digest the reference holds (src/cluster/download.rs:363,
+    `.hidden f 7 6d7f5f98...` = SHA-512/256(b"Hidden\\n")), reproduced by
+    the GPU scan: subdir/.hidden scanned with HashType::sha512_256() emits
+    that line byte for byte."""
+    want = [ln for ln in dirsig_example["index"].encode().split(b"\n")
+            if ln.startswith(b"  .hidden ")]
+    assert len(want) == 1
+    (tmp_path / "subdir").mkdir()
+    (tmp_path / "subdir" / ".hidden").write_bytes(b"Hidden\n")
+    cfg = gpu.ScannerConfig.new().hash(gpu.HashType.sha512_256()).add_dir(str(tmp_path), "/")
+    index = gpu.v1.scan(cfg, context=small_ctx)
+    got = [ln for ln in index.split(b"\n") if ln.startswith(b"  .hidden ")]
+    assert got == want
+    assert index.startswith(b"DIRSIGNATURE.v1 sha512/256 block_size=32768\n/\n/subdir\n")
+    # and through the per-block entry points
+    assert gpu.sha512_256(b"Hidden\n").hex() == want[0].split()[-1].decode()
+
+
+def test_memory_blocks_sha512(gpu, oracle):
+    """register_memory_blocks(HashType::sha512_256(), ..) keys blocks by their
+    SHA-512/256 digests (put-file against a sha512/256 index,
+    src/client/put_file/network.rs:56, src/blocks.rs:187-204)."""
+    data = os.urandom(int(2.5 * 4096))
+    r = gpu.ThreadedBlockReader()
+    r.register_memory_blocks(gpu.HashType.sha512_256(), 4096, data)
+    assert len(r) == 3
+    for i in range(3):
+        blk = data[i * 4096:(i + 1) * 4096]
+        assert r.read_block(oracle_sha(oracle, blk)) == blk
+    with pytest.raises(gpu.ReadError):
+        r.read_block(oracle_digest(oracle, data[:4096]))  # not a blake2b registry
+
+
+def test_current_device_is_preserved(gpu, ctx, small_ctx, tmp_path):
+    """No entry point changes the caller's current HIP device (the header's
+    contract; a NULL stream means the current device's null stream)."""
+    import torch
+    dev = torch.cuda.current_device()
+    data = os.urandom(100000)
+    gpu.BlockHash.hash_bytes(data)
+    assert torch.cuda.current_device() == dev
+    ctx.hash_memory(data, 4096)
+    ctx.hash_blocks(data, [0, 10], [10, 5000])
+    assert torch.cuda.current_device() == dev
+    make_tree(tmp_path)
+    gpu.v1.scan(gpu.ScannerConfig.new().add_dir(str(tmp_path), "/"), context=small_ctx)
+    assert torch.cuda.current_device() == dev
+    c2 = gpu.Context(device_mask=1)
+    c2.close()
+    assert torch.cuda.current_device() == dev
+    # the ordering scratch lives on the stream's device
+    t = torch.tensor(bytearray(data), dtype=torch.uint8, device="cuda:0")
+    off = torch.tensor([0, 4096], dtype=torch.int64, device="cuda:0")
+    ln = torch.tensor([4096, 90000], dtype=torch.int32, device="cuda:0")
+    out = torch.zeros(64, dtype=torch.uint8, device="cuda:0")
+    ctx.hash_blocks_dev(t.data_ptr(), off.data_ptr(), ln.data_ptr(), 2, out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    assert torch.cuda.current_device() == dev
+    assert out.cpu().numpy().tobytes() == gpu.BlockHash.hash_bytes(data[:4096]).__bytes__() + \
+        gpu.BlockHash.hash_bytes(data[4096:94096]).__bytes__()
+
+
+def test_rewrite_rejects_invalid_paths(gpu, small_ctx):
+    """RawIndex::into_mut's InvalidPath (src/cluster/download.rs:143-161) with
+    a real context: `..` / `.` components and names are parse errors."""
+    for bad in (b"/\n/a/../b\n  f f 0\n", b"/\n  .. f 0\n", b"/\n  . s x\n"):
+        idx = b"DIRSIGNATURE.v1 blake2b/256 block_size=32768\n" + bad + b"ab" * 32 + b"\n"
+        with pytest.raises(gpu.CiruelaError) as e:
+            small_ctx.index_rewrite(idx)
+        assert e.value.status == gpu._n.CIR_EPARSE

@@ -7,8 +7,13 @@ stream (seed 0x5EED0004 ^ global index).  Checked here without a GPU:
   * every rank regenerates its blocks from the global index alone, so a
     block's digest does not depend on which rank hashed it (oracle digests of
     boundary blocks computed on both sides agree);
-  * the timing reduction is a MAX over ranks (bench.py's all_reduce).
+  * the timing and the whole-job rate come from bench.py's own functions
+    (timed_steps -> max_over_ranks -> job_rate), run here under gloo with
+    ranks of different speed: the reported time is the slowest rank's;
+  * bench.config4_check, the N>1 bench line's parity check, finds no
+    mismatch on a shard's true digests and every corrupted one.
 """
+import time
 import ctypes
 import os
 import socket
@@ -51,15 +56,26 @@ def _worker(rank, world, port, nblk, q):
     buf = np.empty(count * BS // 8, dtype=np.uint64)
     lib.oracle_splitmix64_fill(buf.ctypes.data, 0, buf.size, SEED_C4, BS // 8, first)
     dig = np.empty(count * 32, dtype=np.uint8)
-    lib.oracle_hash_chunks(buf.ctypes.data, count * BS, BS, dig.ctypes.data, 1)
-    # gather shard bounds and the digest of every rank's first block
-    t = torch.tensor([first, count] + list(dig[:32].astype(np.int64)), dtype=torch.int64)
+    steps = 3
+
+    def step(i):  # the rank's work; rank r is (r + 1) x slower
+        lib.oracle_hash_chunks(buf.ctypes.data, count * BS, BS, dig.ctypes.data, 1)
+        time.sleep(0.05 * (rank + 1))
+    elapsed = bench.timed_steps(step, steps, lambda: None, dist.barrier)
+    elapsed_max = bench.max_over_ranks(elapsed)
+    value = bench.job_rate(count * BS, world, steps, elapsed_max)
+    # bench's N>1 parity check on this shard: clean, then one corrupted digest
+    nbad, checked = bench.config4_check(lib, dig, count * BS, BS, first, sample=8)
+    bad = dig.copy()
+    bad[32 * (count - 1)] ^= 1
+    nbad2, _ = bench.config4_check(lib, bad, count * BS, BS, first, sample=8)
+    # gather shard bounds, timings and the digest of every rank's first block
+    t = torch.tensor([first, count, int(elapsed * 1e9), int(elapsed_max * 1e9), nbad, nbad2,
+                      checked] + list(dig[:32].astype(np.int64)), dtype=torch.int64)
     parts = [torch.zeros_like(t) for _ in range(world)]
     dist.all_gather(parts, t)
-    elapsed = torch.tensor([0.1 * (rank + 1)], dtype=torch.float64)
-    dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     if rank == 0:
-        q.put(([p.tolist() for p in parts], float(elapsed.item())))
+        q.put(([p.tolist() for p in parts], value, elapsed_max))
     dist.destroy_process_group()
 
 
@@ -72,7 +88,7 @@ def test_range_split_gloo(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, nblk, q)) for r in range(world)]
     for p in procs:
         p.start()
-    parts, elapsed = q.get(timeout=120)
+    parts, value, elapsed_max = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -81,11 +97,17 @@ def test_range_split_gloo(world):
     for (a, n), (b, _) in zip(bounds, bounds[1:]):
         assert a + n == b  # contiguous, disjoint
     assert bounds[-1][0] + bounds[-1][1] == world * nblk
-    assert elapsed == pytest.approx(0.1 * world)  # max over ranks
+    # max over ranks: every rank got the same maximum, the slowest rank's
+    # time, at least its 3 x 0.05 * world seconds of sleep
+    assert {p[3] for p in parts} == {max(p[2] for p in parts)}
+    assert elapsed_max >= 3 * 0.05 * world
+    assert value == pytest.approx(nblk * BS * world * 3 / elapsed_max / (1 << 30))
+    for p in parts:
+        assert p[4] == 0 and p[5] == 1 and p[6] >= 8
     # the first block of rank 1 == global block nblk, regenerated from scratch here
     lib = _oracle()
     buf = np.empty(BS // 8, dtype=np.uint64)
     lib.oracle_splitmix64_fill(buf.ctypes.data, 0, buf.size, SEED_C4, BS // 8, nblk)
     dig = np.empty(32, dtype=np.uint8)
     lib.oracle_hash_chunks(buf.ctypes.data, BS, BS, dig.ctypes.data, 1)
-    assert [int(x) for x in dig] == parts[1][2:]
+    assert [int(x) for x in dig] == parts[1][7:]
