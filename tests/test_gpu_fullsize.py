@@ -9,6 +9,7 @@ Config 2 (1 M x 32 KiB = 32 GiB) and config 3 (10 GiB of mixed 4 KiB /
   * determinism: a second launch gives the identical digest array, and the
     per-lane direct loader gives the same array as the LDS-DMA loader.
 """
+import os
 import random
 from concurrent.futures import ThreadPoolExecutor
 
