@@ -218,7 +218,7 @@ def test_scan_tree_above_2gib(gpu, oracle, tmp_path):
     try:
         rng = np.random.default_rng(0x5EED2)
         sizes = [(40 << 20) + 12345, 0, 1, 32767, 32768, 32769, (300 << 20) - 7]
-        sizes += [int(x) for x in rng.integers(1 << 20, 60 << 20, size=56)]
+        sizes += [int(x) for x in rng.integers(1 << 20, 60 << 20, size=72)]
         total = 0
         for i, sz in enumerate(sizes):
             d = os.path.join(top, "d%d" % (i % 5), "e%d" % (i % 3))
