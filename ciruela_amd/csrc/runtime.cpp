@@ -677,11 +677,9 @@ static int single_launch(Device& d, const uint8_t* p, size_t n, uint8_t* out) {
     d.single_cap = cap;
   }
   if (n) memcpy(d.single_h, p, n);
-  uint8_t* h_src = nullptr;
-  uint8_t* h_dst = nullptr;
-  CIR_HIP(hipHostGetDevicePointer((void**)&h_src, d.single_h, 0));
-  CIR_HIP(hipHostGetDevicePointer((void**)&h_dst, d.single_out, 0));
-  CIR_HIP(dev::launch_single(h_src, (uint32_t)n, d.single_d, h_dst, d.single));
+  // pinned host memory is device-accessible at its host address (unified
+  // virtual addressing on ROCm)
+  CIR_HIP(dev::launch_single(d.single_h, (uint32_t)n, d.single_d, d.single_out, d.single));
   CIR_HIP(hipStreamSynchronize(d.single));
   memcpy(out, d.single_out, 32);
   return CIR_OK;
