@@ -378,12 +378,14 @@ hipError_t launch_chain_step(uint64_t* st, const uint8_t* data, uint32_t n, bool
 // loads in flight per lane), then one quad hashes the chain from there
 // (L2-resident, prefetched one line ahead) and writes the 32-byte digest
 // straight into device-mapped host memory.  No staging copies, no ordering
-// kernel, no D2H copy: one launch per call.
+// kernel, no D2H copy: one launch per call.  src == scratch: the bytes are
+// already in device memory (inputs above kSinglePull, uploaded by SDMA, which
+// moves them faster than one workgroup's PCIe reads).
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_single(
     const uint8_t* __restrict__ src, uint32_t n, uint8_t* __restrict__ scratch,
     uint8_t* __restrict__ dout) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[128];
-  const uint32_t nv = (n + 15u) >> 4;  // 16-B vectors (src/scratch hold whole vectors)
+  const uint32_t nv = src == scratch ? 0u : (n + 15u) >> 4;  // 16-B vectors to pull
   const uint4* s4 = reinterpret_cast<const uint4*>(src);
   uint4* d4 = reinterpret_cast<uint4*>(scratch);
   for (uint32_t v = threadIdx.x; v < nv; v += 4u * kThreads) {
@@ -403,6 +405,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
   __syncthreads();
   const uint32_t i = threadIdx.x;
   if (i >= 4) return;
+  __builtin_amdgcn_s_setprio(3);
   uint32_t addr[48];
   quad_addr(addr, 0u, i);
   uint64_t h0, h1;

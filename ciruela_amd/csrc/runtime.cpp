@@ -652,6 +652,8 @@ int cir_hash_blocks(cir_ctx* ctx, const uint8_t* h_arena, const uint64_t* off,
 // a larger input runs for milliseconds, so the staged path's fixed cost no
 // longer matters there.
 constexpr size_t kSingleMax = 16ull << 20;
+// Up to this size the kernel reads the pinned input itself (one launch).
+constexpr size_t kSinglePull = 64ull << 10;
 
 // BlockHash::hash_bytes in one kernel launch: copy into a pinned buffer the
 // GPU reads over PCIe, launch, wait, read the digest the kernel wrote into
@@ -678,8 +680,14 @@ static int single_launch(Device& d, const uint8_t* p, size_t n, uint8_t* out) {
   }
   if (n) memcpy(d.single_h, p, n);
   // pinned host memory is device-accessible at its host address (unified
-  // virtual addressing on ROCm)
-  CIR_HIP(dev::launch_single(d.single_h, (uint32_t)n, d.single_d, d.single_out, d.single));
+  // virtual addressing on ROCm).  Small inputs are pulled over PCIe by the
+  // kernel itself (no copy launch); larger ones go up by one SDMA copy first.
+  const uint8_t* src = d.single_h;
+  if (n > kSinglePull) {
+    CIR_HIP(hipMemcpyAsync(d.single_d, d.single_h, need, hipMemcpyHostToDevice, d.single));
+    src = d.single_d;
+  }
+  CIR_HIP(dev::launch_single(src, (uint32_t)n, d.single_d, d.single_out, d.single));
   CIR_HIP(hipStreamSynchronize(d.single));
   memcpy(out, d.single_out, 32);
   return CIR_OK;
