@@ -656,20 +656,22 @@ hipError_t launch_general_desc(const uint8_t* arena, const uint64_t* off, const 
 
 hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
                         const uint32_t* perm, const uint32_t* n_long, uint64_t n, uint8_t* out,
-                        hipStream_t s, hipStream_t aux, hipEvent_t fork, hipEvent_t join) {
+                        hipStream_t s, hipStream_t qs, hipStream_t aux, hipEvent_t fork,
+                        hipEvent_t qjoin, hipEvent_t ljoin) {
   if (n == 0) return hipSuccess;
   const uint64_t nq = std::min<uint64_t>((n + 63) / 64, quad_max_wg(n));
   const uint64_t lane_grid = grid_for(n, kThreads);
   if (lane_grid > 0x7fffffffull) return hipErrorInvalidValue;
   const bool exclusive = CIR_QUAD_EXCLUSIVE && n >= kQuadSmallBatch;
   hipError_t e = hipEventRecord(fork, s);
+  if (e == hipSuccess) e = hipStreamWaitEvent(qs, fork, 0);
   if (e == hipSuccess) e = hipStreamWaitEvent(aux, fork, 0);
   if (e != hipSuccess) return e;
   if (exclusive) {
     // The quad workgroups need whole CUs (one 504-register wave per SIMD):
     // they are dispatched first, and the lane part starts ~20 us later, so
     // its waves fill the other CUs instead of taking every SIMD first.
-    hipLaunchKernelGGL((k_quad_long<kQuadAsm, true>), dim3((unsigned)nq), dim3(kThreads), 0, s,
+    hipLaunchKernelGGL((k_quad_long<kQuadAsm, true>), dim3((unsigned)nq), dim3(kThreads), 0, qs,
                        arena, off, len, perm, n_long, (uint32_t)nq, out);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -683,12 +685,14 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
                        len, perm, n, n_long, (uint32_t)nq, out);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_quad_long<kQuadAsm, false>), dim3((unsigned)nq), dim3(kThreads), 0, s,
+    hipLaunchKernelGGL((k_quad_long<kQuadAsm, false>), dim3((unsigned)nq), dim3(kThreads), 0, qs,
                        arena, off, len, perm, n_long, (uint32_t)nq, out);
   }
   e = hipGetLastError();
-  if (e == hipSuccess) e = hipEventRecord(join, aux);
-  if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
+  if (e == hipSuccess) e = hipEventRecord(qjoin, qs);
+  if (e == hipSuccess) e = hipEventRecord(ljoin, aux);
+  if (e == hipSuccess) e = hipStreamWaitEvent(s, qjoin, 0);
+  if (e == hipSuccess) e = hipStreamWaitEvent(s, ljoin, 0);
   return e;
 }
 

@@ -62,12 +62,13 @@ hipError_t launch_general_desc(const uint8_t* arena, const uint64_t* off, const 
                                const uint32_t* perm, uint64_t n, uint8_t* out, hipStream_t s);
 
 // Descriptor batch in the order perm (longest chain first); the first
-// min(*n_long, 64 * quad_max_wg(n)) chains (device count) run in quad mode on s,
-// the rest one lane per chain on `aux` (forked from s with `fork`, joined
-// back into s with `join`).
+// min(*n_long, 64 * quad_max_wg(n)) chains (device count) run in quad mode on
+// qs, the rest one lane per chain on `aux`; both fork from s (`fork`) and
+// join back into s (`qjoin`, `ljoin`).
 hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
                         const uint32_t* perm, const uint32_t* n_long, uint64_t n, uint8_t* out,
-                        hipStream_t s, hipStream_t aux, hipEvent_t fork, hipEvent_t join);
+                        hipStream_t s, hipStream_t qs, hipStream_t aux, hipEvent_t fork,
+                        hipEvent_t qjoin, hipEvent_t ljoin);
 
 // Longest-chain-first order of a descriptor batch (order.hip): *perm points
 // into `scratch` (order_scratch_bytes(n) bytes, device memory).

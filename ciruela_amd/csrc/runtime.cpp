@@ -58,9 +58,12 @@ Device::~Device() {
   (void)hipFree(order_scratch);
   if (order_free) (void)hipEventDestroy(order_free);
   if (aux) (void)hipStreamSynchronize(aux);
+  if (qstream) (void)hipStreamSynchronize(qstream);
   if (aux_fork) (void)hipEventDestroy(aux_fork);
   if (aux_join) (void)hipEventDestroy(aux_join);
+  if (q_join) (void)hipEventDestroy(q_join);
   if (aux) (void)hipStreamDestroy(aux);
+  if (qstream) (void)hipStreamDestroy(qstream);
   if (single) (void)hipStreamSynchronize(single);
   (void)hipHostFree(single_h);
   (void)hipHostFree(single_out);
@@ -123,6 +126,21 @@ int Device::ensure_slot(Slot& s, uint64_t bytes, uint64_t nblk) {
   return CIR_OK;
 }
 
+// A stream on its own hardware queue: a CU-masked stream (here the full
+// mask) is created on a queue of its own rather than one of the process's
+// GPU_MAX_HW_QUEUES shared ones.  CIR_SHARED_PART_QUEUES=1 falls back to
+// plain streams (A/B measurements).
+static hipError_t create_part_stream(int dev_id, hipStream_t* s) {
+  if (const char* v = std::getenv("CIR_SHARED_PART_QUEUES"))
+    if (*v && strcmp(v, "0") != 0) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+  hipDeviceProp_t prop;
+  hipError_t e = hipGetDeviceProperties(&prop, dev_id);
+  if (e != hipSuccess) return e;
+  std::vector<uint32_t> mask((prop.multiProcessorCount + 31) / 32, 0u);
+  for (int c = 0; c < prop.multiProcessorCount; ++c) mask[c / 32] |= 1u << (c % 32);
+  return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
+}
+
 // Descriptor batch, longest chain first: device sort (order.hip) into the
 // device's ordering scratch, then the general kernel through the permutation.
 bool valid_hash_type(int ht) { return ht == CIR_HASH_BLAKE2B_256 || ht == CIR_HASH_SHA512_256; }
@@ -142,9 +160,11 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
   const size_t need = dev::order_scratch_bytes(n);
   if (!d.order_free) {
     CIR_HIP(hipEventCreateWithFlags(&d.order_free, hipEventDisableTiming));
-    CIR_HIP(hipStreamCreateWithFlags(&d.aux, hipStreamNonBlocking));
+    CIR_HIP(create_part_stream(d.id, &d.qstream));
+    CIR_HIP(create_part_stream(d.id, &d.aux));
     CIR_HIP(hipEventCreateWithFlags(&d.aux_fork, hipEventDisableTiming));
     CIR_HIP(hipEventCreateWithFlags(&d.aux_join, hipEventDisableTiming));
+    CIR_HIP(hipEventCreateWithFlags(&d.q_join, hipEventDisableTiming));
   }
   if (need > d.order_cap) {
     CIR_HIP(hipEventSynchronize(d.order_free));
@@ -161,8 +181,8 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
   if (ht == CIR_HASH_SHA512_256)
     CIR_HIP(dev::launch_sha_desc(arena, off, len, perm, n, out, s));
   else
-    CIR_HIP(dev::launch_mixed(arena, off, len, perm, n_long, n, out, s, d.aux, d.aux_fork,
-                              d.aux_join));
+    CIR_HIP(dev::launch_mixed(arena, off, len, perm, n_long, n, out, s, d.qstream, d.aux,
+                              d.aux_fork, d.q_join, d.aux_join));
   CIR_HIP(hipEventRecord(d.order_free, s));
   return CIR_OK;
 }

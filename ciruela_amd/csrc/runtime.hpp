@@ -82,9 +82,14 @@ struct Device {
   void* order_scratch = nullptr;
   size_t order_cap = 0;
   hipEvent_t order_free = nullptr;
-  // lane part of an ordered batch runs on `aux`, forked/joined by events
-  hipStream_t aux = nullptr;
-  hipEvent_t aux_fork = nullptr, aux_join = nullptr;
+  // An ordered batch forks from the caller's stream onto two streams of our
+  // own, the quad part on `qstream`, the lane part on `aux`, and joins back
+  // (events).  Both are created with a full CU mask, which gives each its own
+  // hardware queue: the two parts run concurrently whatever queue the
+  // caller's stream shares (with GPU_MAX_HW_QUEUES = 4 and a few contexts in
+  // one process, ordinary streams share queues and the parts serialised).
+  hipStream_t aux = nullptr, qstream = nullptr;
+  hipEvent_t aux_fork = nullptr, aux_join = nullptr, q_join = nullptr;
   // incremental footer chain (cir_scan_v1): own stream, state, text buffers
   std::mutex chain_mu;  // one incremental footer (scan) at a time per device
   hipStream_t chain = nullptr;
