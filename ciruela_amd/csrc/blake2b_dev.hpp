@@ -586,57 +586,6 @@ __device__ __forceinline__ void compress_quad_asm(uint64_t& a, uint64_t& b, uint
                : "vcc");
 }
 
-// A whole compression AND its finalisation in one block, the chain value
-// pinned: h0 -> v[52:53], h1 -> v[54:55], cv = IV[i] -> v[56:57], dv =
-// IV[4+i] ^ t / f contribution -> v[58:59].  The first G reads h0, h1, cv
-// and dv where they are (no copies into a, b, c, d), and the finalisation
-// h0 ^= a ^ c(lane i+2), h1 ^= b(lane i+3) ^ d(lane i+1) is 8 VOP2/DPP
-// instructions ordered so that no DPP source is read within 2 instructions
-// of its write (c is read first; b, written last, 4 instructions later).
-// 536 VALU instructions per compression, no moves, no s_nop.
-#define CIR_QG_FIRST(X, Y)                                                    \
-  "v_lshl_add_u64 v[40:41], v[52:53], 0, " X "\n"                             \
-  "v_lshl_add_u64 v[40:41], v[40:41], 0, v[54:55]\n"                          \
-  "v_xor_b32 v48, v59, v41\n"                                                 \
-  "v_xor_b32 v49, v58, v40\n"                                                 \
-  "v_lshl_add_u64 v[44:45], v[56:57], 0, v[48:49]\n"                          \
-  "v_xor_b32 v50, v54, v44\n"                                                 \
-  "v_xor_b32 v51, v55, v45\n"                                                 \
-  "v_alignbit_b32 v42, v51, v50, 24\n"                                        \
-  "v_alignbit_b32 v43, v50, v51, 24\n" CIR_QG_TAIL(Y)
-#define CIR_QFINAL                                                            \
-  "v_xor_b32_dpp v48, v44, v40" CIR_QP_4E "\n"                                \
-  "v_xor_b32_dpp v49, v45, v41" CIR_QP_4E "\n"                                \
-  "v_xor_b32 v52, v52, v48\n"                                                 \
-  "v_xor_b32 v53, v53, v49\n"                                                 \
-  "v_xor_b32_dpp v54, v42, v54" CIR_QP_93 "\n"                                \
-  "v_xor_b32_dpp v55, v43, v55" CIR_QP_93 "\n"                                \
-  "v_xor_b32_dpp v54, v46, v54" CIR_QP_39 "\n"                                \
-  "v_xor_b32_dpp v55, v47, v55" CIR_QP_39 "\n"
-#define CIR_QCOMPRESS_FULL                                                    \
-  CIR_QG_FIRST(CIR_M(0), CIR_M(1))                                            \
-  CIR_QG_DPP(CIR_QP_39, CIR_QP_4E, CIR_QP_93, CIR_M(2), CIR_M(3))             \
-  CIR_QR(4, 5, 6, 7) CIR_QR(8, 9, 10, 11) CIR_QR(12, 13, 14, 15)              \
-  CIR_QR(16, 17, 18, 19) CIR_QR(20, 21, 22, 23) CIR_QR(24, 25, 26, 27)        \
-  CIR_QR(28, 29, 30, 31) CIR_QR(32, 33, 34, 35) CIR_QR(36, 37, 38, 39)        \
-  CIR_QR(0, 1, 2, 3) CIR_QR(4, 5, 6, 7) CIR_QFINAL
-
-__device__ __forceinline__ void compress_quad_full(uint64_t& h0, uint64_t& h1, uint64_t cv,
-                                                   uint64_t dv, const uint64_t (&m)[40]) {
-  uint64_t a, b, c, d, t, u;
-  asm volatile(CIR_QCOMPRESS_FULL
-               : "+{v[52:53]}"(h0), "+{v[54:55]}"(h1), "=&{v[40:41]}"(a), "=&{v[42:43]}"(b),
-                 "=&{v[44:45]}"(c), "=&{v[46:47]}"(d), "=&{v[48:49]}"(t), "=&{v[50:51]}"(u)
-               : "{v[56:57]}"(cv), "{v[58:59]}"(dv), CIR_MO(0), CIR_MO(1), CIR_MO(2), CIR_MO(3),
-                 CIR_MO(4), CIR_MO(5), CIR_MO(6), CIR_MO(7), CIR_MO(8), CIR_MO(9), CIR_MO(10),
-                 CIR_MO(11), CIR_MO(12), CIR_MO(13), CIR_MO(14), CIR_MO(15), CIR_MO(16),
-                 CIR_MO(17), CIR_MO(18), CIR_MO(19), CIR_MO(20), CIR_MO(21), CIR_MO(22),
-                 CIR_MO(23), CIR_MO(24), CIR_MO(25), CIR_MO(26), CIR_MO(27), CIR_MO(28),
-                 CIR_MO(29), CIR_MO(30), CIR_MO(31), CIR_MO(32), CIR_MO(33), CIR_MO(34),
-                 CIR_MO(35), CIR_MO(36), CIR_MO(37), CIR_MO(38), CIR_MO(39)
-               : "vcc");
-}
-
 // One round of quad mode: column step (words x0, y0), diagonal step (x1, y1).
 // kFirst: round 0 (state in the column layout); kLast: round 11.
 template <bool kFirst, bool kLast>

@@ -179,111 +179,6 @@ __device__ __forceinline__ void quad_init(uint32_t i, uint64_t& h0, uint64_t& h1
   h1 = iv_hi(i);
 }
 
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
-  return __builtin_amdgcn_readfirstlane(v);
-}
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
-  return __builtin_amdgcn_readfirstlane(v);
-}
-
-// Pipelined quad mode (the production path; every lane of the wave must
-// execute it, t0 must be wave-uniform).  Line it+1 goes global -> regs ->
-// LDS -> the other message set (ma / mb) while line it compresses: at the
-// top of each half the previous reads have landed (lgkmcnt(0)), so the LDS
-// line is free for the next write and the asm's operands need no wait; the
-// next set's 40 reads stay in flight across the compression.
-//
-// The loop is wave-uniform: it runs to the longest chain of the wave, and
-// while no lane is at its last line (it + 1 < tmin) a step is the bare
-// compression -- t is a scalar, the lane's t / final contribution one
-// and-xor, no per-lane branches or exec masking -- and while every lane's
-// next line is whole and 16-B aligned (it < ffast) the fetch is two
-// unconditional 16-B loads.  Only the last lines of the wave's chains take
-// the general step (per-lane t, final flag, state kept where a chain has
-// ended).  Quads without a chain (active = false) run quad 0's chain of the
-// wave, in bounds, and store nothing.  Per compression: the 536-instruction
-// asm block (compression + finalisation) and ~50 instructions of glue, the
-// 40 LDS reads most of it.
-__device__ __forceinline__ void quad_run_pipe(uint64_t& h0, uint64_t& h1, uint64_t t0,
-                                              const uint8_t* p, uint32_t L, bool active,
-                                              bool final, uint8_t* lds,
-                                              const uint32_t (&addr)[48], uint32_t line,
-                                              uint32_t i) {
-  {
-    const int src = (int)i;  // lane i of quad 0
-    const uint64_t pv = reinterpret_cast<uintptr_t>(p);
-    const uint32_t plo = (uint32_t)__shfl((int)(uint32_t)pv, src);
-    const uint32_t phi = (uint32_t)__shfl((int)(uint32_t)(pv >> 32), src);
-    const uint32_t L0 = (uint32_t)__shfl((int)L, src);
-    if (!active) {
-      // moved by an offset, not rebuilt from an integer: p keeps its
-      // (global) address space, so its loads stay global_load, not flat
-      p += (int64_t)((((uint64_t)phi << 32) | plo) - pv);
-      L = L0;
-    }
-  }
-  const uint32_t nfull = L >> 7, rem = L & 127u;
-  const uint32_t total =
-      final ? nfull + ((rem != 0u || (L == 0u && t0 == 0u)) ? 1u : 0u) : nfull;
-  const bool al16 = (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
-  const uint32_t tmin = wave_min_u32(total), tmax = wave_max_u32(total);
-  const uint32_t ffast = wave_min_u32(al16 ? nfull : 0u);
-  if (tmax == 0) return;
-  const uint64_t cv = iv_lo(i), dv0 = iv_hi(i);
-  const uint64_t dmask = i == 0 ? ~0ull : 0ull;
-  auto fetch = [&](uint32_t it, uint4& u, uint4& w) {
-    const uint8_t* q = p + (uint64_t)it * 128u + 32u * i;
-    if (it < ffast) {
-      u = reinterpret_cast<const uint4*>(q)[0];
-      w = reinterpret_cast<const uint4*>(q)[1];
-    } else {
-      const uint32_t lb = it < nfull ? 128u : it == nfull ? rem : 0u;
-      const uint32_t n = lb > 32u * i ? min(32u, lb - 32u * i) : 0u;
-      load32_safe(u, w, q, n, al16);
-    }
-  };
-  uint64_t ma[40], mb[40];
-  uint4 u, w;
-  fetch(0, u, w);
-  auto stage = [&](uint32_t it, uint64_t (&m)[40]) {
-    *reinterpret_cast<uint4*>(lds + line + 32u * i) = u;
-    *reinterpret_cast<uint4*>(lds + line + 32u * i + 16u) = w;
-    if (it + 1 < tmax) fetch(it + 1, u, w);
-    quad_read_msg(m, lds, addr);
-  };
-  auto step = [&](uint32_t it, const uint64_t (&m)[40]) {
-    if (it + 1 < tmin) {
-      const uint64_t t = t0 + (uint64_t)(it + 1) * 128u;
-      compress_quad_full(h0, h1, cv, dv0 ^ (t & dmask), m);
-    } else {
-      const bool last = final && it + 1 == total;
-      const uint64_t t = t0 + (last ? (uint64_t)L : (uint64_t)(it + 1) * 128u);
-      const uint64_t dv = dv0 ^ (i == 0 ? t : 0ull) ^ ((i == 2 && last) ? ~0ull : 0ull);
-      uint64_t g0 = h0, g1 = h1;
-      compress_quad_full(g0, g1, cv, dv, m);
-      if (it < total) {
-        h0 = g0;
-        h1 = g1;
-      }
-    }
-  };
-  constexpr int kLgkm0 = 0xC07F;  // s_waitcnt lgkmcnt(0), vmcnt/expcnt untouched
-  stage(0, ma);
-  for (uint32_t it = 0; it < tmax; it += 2) {
-    __builtin_amdgcn_s_waitcnt(kLgkm0);
-    if (it + 1 < tmax) stage(it + 1, mb);
-    step(it, ma);
-    if (it + 1 >= tmax) break;
-    __builtin_amdgcn_s_waitcnt(kLgkm0);
-    if (it + 2 < tmax) stage(it + 2, ma);
-    step(it + 1, mb);
-  }
-}
-
 // Advance a quad's chain over L bytes at p, t0 bytes already compressed.
 // final: the last line (partial, or the empty block of an empty input)
 // carries the final flag; otherwise L must be a multiple of 128.
@@ -302,12 +197,42 @@ __device__ __forceinline__ void quad_run(uint64_t& h0, uint64_t& h1, uint64_t t0
     const uint32_t n = lb > 32u * i ? min(32u, lb - 32u * i) : 0u;
     load32_safe(u, w, p + (uint64_t)it * 128u + 32u * i, n, al16);
   };
-  if constexpr (kAsm && kPrefetchAll) {
-    quad_run_pipe(h0, h1, t0, p, L, active, final, lds, addr, line, i);
-    return;
-  }
   uint4 u = make_uint4(0, 0, 0, 0), w = u;
   if (total) fetch(0, u, w);
+  if constexpr (kAsm && kPrefetchAll) {
+    // Pipelined: line it+1 goes regs -> LDS -> the other message set (ma /
+    // mb) while line it compresses.  At the top of each half the previous
+    // reads have landed (lgkmcnt(0)), so the LDS line is free for the next
+    // write and the asm's operands need no wait; the next set's 40 reads
+    // stay in flight across the compression (the asm names only the current
+    // set).  A compression no longer waits on the LDS round trip (write, 40
+    // reads: ~300-500 cycles for a wave alone).
+    uint64_t ma[40], mb[40];
+    auto stage = [&](uint32_t it, uint64_t (&m)[40]) {
+      *reinterpret_cast<uint4*>(lds + line + 32u * i) = u;
+      *reinterpret_cast<uint4*>(lds + line + 32u * i + 16u) = w;
+      if (it + 1 < total) fetch(it + 1, u, w);
+      quad_read_msg(m, lds, addr);
+    };
+    auto step = [&](uint32_t it, const uint64_t (&m)[40]) {
+      const bool last = final && it + 1 == total;
+      const uint64_t t = t0 + (last ? (uint64_t)L : (uint64_t)(it + 1) * 128u);
+      const uint64_t dv = dv0 ^ (i == 0 ? t : 0ull) ^ ((i == 2 && last) ? ~0ull : 0ull);
+      compress_quad_regs(h0, h1, m, cv, dv);
+    };
+    constexpr int kLgkm0 = 0xC07F;  // s_waitcnt lgkmcnt(0), vmcnt/expcnt untouched
+    if (total) stage(0, ma);
+    for (uint32_t it = 0; it < total; it += 2) {
+      __builtin_amdgcn_s_waitcnt(kLgkm0);
+      if (it + 1 < total) stage(it + 1, mb);
+      step(it, ma);
+      if (it + 1 >= total) break;
+      __builtin_amdgcn_s_waitcnt(kLgkm0);
+      if (it + 2 < total) stage(it + 2, ma);
+      step(it + 1, mb);
+    }
+    return;
+  }
   for (uint32_t it = 0; it < total; ++it) {
     // publish this lane's 32 bytes of the line to its quad (LDS is in order
     // per wave: the previous compression's reads precede these writes)
@@ -423,25 +348,20 @@ __global__ __launch_bounds__(kThreads, 4) void k_lane_rest(const uint8_t* __rest
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_chain_step(uint64_t* __restrict__ st,
                                                    const uint8_t* __restrict__ data, uint32_t n,
                                                    int final) {
-  // every quad of the wave runs the chain (quad_run_pipe is wave-uniform);
-  // quad 0 stores it
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kQuadWaveLds];
-  const uint32_t lane = threadIdx.x, i = lane & 3u, line = (lane >> 2) * 128u;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[128];
+  const uint32_t i = threadIdx.x;
+  if (i >= 4) return;
   uint32_t addr[48];
-  quad_addr(addr, line, i);
-  const uint64_t t0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(st[8] >> 32)) << 32) |
-                      __builtin_amdgcn_readfirstlane((uint32_t)st[8]);
-  const uint32_t fresh = __builtin_amdgcn_readfirstlane((uint32_t)st[9]) == 0u && t0 == 0;
+  quad_addr(addr, 0u, i);
+  const uint64_t t0 = st[8];
   uint64_t h0 = st[i], h1 = st[4 + i];
-  if (fresh) quad_init(i, h0, h1);  // st[9] = 0: fresh state
-  quad_run<true>(h0, h1, t0, data, n, true, final != 0, lds, addr, line, i);
-  if (lane < 4) {
-    st[i] = h0;
-    st[4 + i] = h1;
-    if (i == 0) {
-      st[8] = t0 + n;
-      st[9] = 1;
-    }
+  if (t0 == 0 && st[9] == 0) quad_init(i, h0, h1);  // st[9] = 0: fresh state
+  quad_run<true>(h0, h1, t0, data, n, true, final != 0, lds, addr, 0u, i);
+  st[i] = h0;
+  st[4 + i] = h1;
+  if (i == 0) {
+    st[8] = t0 + n;
+    st[9] = 1;
   }
 }
 
@@ -464,7 +384,7 @@ hipError_t launch_chain_step(uint64_t* st, const uint8_t* data, uint32_t n, bool
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_single(
     const uint8_t* __restrict__ src, uint32_t n, uint8_t* __restrict__ scratch,
     uint8_t* __restrict__ dout) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kQuadWaveLds];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[128];
   const uint32_t nv = src == scratch ? 0u : (n + 15u) >> 4;  // 16-B vectors to pull
   const uint4* s4 = reinterpret_cast<const uint4*>(src);
   uint4* d4 = reinterpret_cast<uint4*>(scratch);
@@ -483,15 +403,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
   }
   __threadfence_block();
   __syncthreads();
-  if (threadIdx.x >= 64) return;  // wave 0 hashes (every quad the same chain)
+  const uint32_t i = threadIdx.x;
+  if (i >= 4) return;
   __builtin_amdgcn_s_setprio(3);
-  const uint32_t lane = threadIdx.x, i = lane & 3u, line = (lane >> 2) * 128u;
   uint32_t addr[48];
-  quad_addr(addr, line, i);
+  quad_addr(addr, 0u, i);
   uint64_t h0, h1;
   quad_init(i, h0, h1);
-  quad_run<true>(h0, h1, 0, scratch, n, true, true, lds, addr, line, i);
-  if (lane < 4) reinterpret_cast<uint64_t*>(dout)[i] = h0;
+  quad_run<true>(h0, h1, 0, scratch, n, true, true, lds, addr, 0u, i);
+  reinterpret_cast<uint64_t*>(dout)[i] = h0;
 }
 
 hipError_t launch_single(const uint8_t* h_src, uint32_t n, uint8_t* d_scratch, uint8_t* h_out,
@@ -664,7 +584,7 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
   if (lane_grid > 0x7fffffffull) return hipErrorInvalidValue;
   const bool exclusive = CIR_QUAD_EXCLUSIVE && n >= kQuadSmallBatch;
   hipError_t e = hipEventRecord(fork, s);
-  if (e == hipSuccess) e = hipStreamWaitEvent(qs, fork, 0);
+  if (e == hipSuccess && qs != s) e = hipStreamWaitEvent(qs, fork, 0);
   if (e == hipSuccess) e = hipStreamWaitEvent(aux, fork, 0);
   if (e != hipSuccess) return e;
   if (exclusive) {
@@ -689,9 +609,9 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
                        arena, off, len, perm, n_long, (uint32_t)nq, out);
   }
   e = hipGetLastError();
-  if (e == hipSuccess) e = hipEventRecord(qjoin, qs);
+  if (e == hipSuccess && qs != s) e = hipEventRecord(qjoin, qs);
   if (e == hipSuccess) e = hipEventRecord(ljoin, aux);
-  if (e == hipSuccess) e = hipStreamWaitEvent(s, qjoin, 0);
+  if (e == hipSuccess && qs != s) e = hipStreamWaitEvent(s, qjoin, 0);
   if (e == hipSuccess) e = hipStreamWaitEvent(s, ljoin, 0);
   return e;
 }

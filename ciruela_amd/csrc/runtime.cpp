@@ -126,13 +126,25 @@ int Device::ensure_slot(Slot& s, uint64_t bytes, uint64_t nblk) {
   return CIR_OK;
 }
 
-// A stream on its own hardware queue: a CU-masked stream (here the full
-// mask) is created on a queue of its own rather than one of the process's
-// GPU_MAX_HW_QUEUES shared ones.  CIR_SHARED_PART_QUEUES=1 falls back to
-// plain streams (A/B measurements).
-static hipError_t create_part_stream(int dev_id, hipStream_t* s) {
-  if (const char* v = std::getenv("CIR_SHARED_PART_QUEUES"))
-    if (*v && strcmp(v, "0") != 0) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+// Where the two parts of an ordered batch run (CIR_PART_STREAMS, read when
+// a device first orders a batch; A/B measurements, tools/queue_probe.py):
+//   own1 (default): quad part on the caller's stream, lane part on a
+//        CU-masked stream -- a CU-masked stream gets a hardware queue of its
+//        own instead of one of the process's GPU_MAX_HW_QUEUES shared ones,
+//        so the lane part can never queue behind the quad part;
+//   own2: both parts on CU-masked streams of their own;
+//   plain: quad part on the caller's stream, lane part on a plain stream
+//        (round 1: the two serialised whenever they shared a queue).
+enum PartMode { kPartOwn1 = 0, kPartOwn2 = 1, kPartPlain = 2 };
+static int part_mode() {
+  const char* v = std::getenv("CIR_PART_STREAMS");
+  if (v && strcmp(v, "own2") == 0) return kPartOwn2;
+  if (v && strcmp(v, "plain") == 0) return kPartPlain;
+  return kPartOwn1;
+}
+
+static hipError_t create_part_stream(int dev_id, bool own_queue, hipStream_t* s) {
+  if (!own_queue) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
   hipDeviceProp_t prop;
   hipError_t e = hipGetDeviceProperties(&prop, dev_id);
   if (e != hipSuccess) return e;
@@ -160,8 +172,9 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
   const size_t need = dev::order_scratch_bytes(n);
   if (!d.order_free) {
     CIR_HIP(hipEventCreateWithFlags(&d.order_free, hipEventDisableTiming));
-    CIR_HIP(create_part_stream(d.id, &d.qstream));
-    CIR_HIP(create_part_stream(d.id, &d.aux));
+    d.part_mode = part_mode();
+    if (d.part_mode == kPartOwn2) CIR_HIP(create_part_stream(d.id, true, &d.qstream));
+    CIR_HIP(create_part_stream(d.id, d.part_mode != kPartPlain, &d.aux));
     CIR_HIP(hipEventCreateWithFlags(&d.aux_fork, hipEventDisableTiming));
     CIR_HIP(hipEventCreateWithFlags(&d.aux_join, hipEventDisableTiming));
     CIR_HIP(hipEventCreateWithFlags(&d.q_join, hipEventDisableTiming));
@@ -181,8 +194,8 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
   if (ht == CIR_HASH_SHA512_256)
     CIR_HIP(dev::launch_sha_desc(arena, off, len, perm, n, out, s));
   else
-    CIR_HIP(dev::launch_mixed(arena, off, len, perm, n_long, n, out, s, d.qstream, d.aux,
-                              d.aux_fork, d.q_join, d.aux_join));
+    CIR_HIP(dev::launch_mixed(arena, off, len, perm, n_long, n, out, s,
+                              d.qstream ? d.qstream : s, d.aux, d.aux_fork, d.q_join, d.aux_join));
   CIR_HIP(hipEventRecord(d.order_free, s));
   return CIR_OK;
 }

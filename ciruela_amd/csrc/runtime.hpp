@@ -82,12 +82,13 @@ struct Device {
   void* order_scratch = nullptr;
   size_t order_cap = 0;
   hipEvent_t order_free = nullptr;
-  // An ordered batch forks from the caller's stream onto two streams of our
-  // own, the quad part on `qstream`, the lane part on `aux`, and joins back
-  // (events).  Both are created with a full CU mask, which gives each its own
-  // hardware queue: the two parts run concurrently whatever queue the
-  // caller's stream shares (with GPU_MAX_HW_QUEUES = 4 and a few contexts in
-  // one process, ordinary streams share queues and the parts serialised).
+  // An ordered batch runs its lane part on `aux` (and, in part mode own2,
+  // its quad part on `qstream`; otherwise on the caller's stream), forked
+  // from and joined back into the caller's stream with events.  aux is
+  // CU-masked, which gives it a hardware queue of its own: the two parts run
+  // concurrently whatever queue the caller's stream shares (runtime.cpp
+  // part_mode).
+  int part_mode = 0;
   hipStream_t aux = nullptr, qstream = nullptr;
   hipEvent_t aux_fork = nullptr, aux_join = nullptr, q_join = nullptr;
   // incremental footer chain (cir_scan_v1): own stream, state, text buffers

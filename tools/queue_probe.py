@@ -5,8 +5,8 @@ its first ordered batch the quad-part / lane-part streams).  With
 GPU_MAX_HW_QUEUES = 4 (HIP's default) ordinary streams of a process share
 hardware queues, and when the quad and lane parts of a mixed batch landed on
 one queue they ran one after the other (r01: 570-610 GiB/s instead of ~850).
-The part streams are now CU-masked (a queue of their own);
-CIR_SHARED_PART_QUEUES=1 restores plain streams for the A/B.
+CIR_PART_STREAMS = own1 (default: lane part on a CU-masked stream, i.e. a
+queue of its own) / own2 (both parts on CU-masked streams) / plain (round 1).
 
     python tools/queue_probe.py --contexts 4 [--steps 10]
 """
@@ -59,8 +59,8 @@ def main():
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
     hashed = int(lens.astype("int64").sum())
-    print("config3 contexts=%d shared_part_queues=%s: %.3f ms  %.1f GiB/s" % (
-        args.contexts, os.environ.get("CIR_SHARED_PART_QUEUES", "0"), dt * 1e3,
+    print("config3 contexts=%d part_streams=%s: %.3f ms  %.1f GiB/s" % (
+        args.contexts, os.environ.get("CIR_PART_STREAMS", "own1"), dt * 1e3,
         hashed / dt / (1 << 30)), flush=True)
 
 
