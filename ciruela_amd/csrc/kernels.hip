@@ -585,7 +585,7 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
   const bool exclusive = CIR_QUAD_EXCLUSIVE && n >= kQuadSmallBatch;
   hipError_t e = hipEventRecord(fork, s);
   if (e == hipSuccess && qs != s) e = hipStreamWaitEvent(qs, fork, 0);
-  if (e == hipSuccess) e = hipStreamWaitEvent(aux, fork, 0);
+  if (e == hipSuccess && aux != s) e = hipStreamWaitEvent(aux, fork, 0);
   if (e != hipSuccess) return e;
   if (exclusive) {
     // The quad workgroups need whole CUs (one 504-register wave per SIMD):
@@ -610,9 +610,9 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
   }
   e = hipGetLastError();
   if (e == hipSuccess && qs != s) e = hipEventRecord(qjoin, qs);
-  if (e == hipSuccess) e = hipEventRecord(ljoin, aux);
+  if (e == hipSuccess && aux != s) e = hipEventRecord(ljoin, aux);
   if (e == hipSuccess && qs != s) e = hipStreamWaitEvent(s, qjoin, 0);
-  if (e == hipSuccess) e = hipStreamWaitEvent(s, ljoin, 0);
+  if (e == hipSuccess && aux != s) e = hipStreamWaitEvent(s, ljoin, 0);
   return e;
 }
 

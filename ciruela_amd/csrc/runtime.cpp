@@ -127,30 +127,45 @@ int Device::ensure_slot(Slot& s, uint64_t bytes, uint64_t nblk) {
 }
 
 // Where the two parts of an ordered batch run (CIR_PART_STREAMS, read when
-// a device first orders a batch; A/B measurements, tools/queue_probe.py):
-//   own1 (default): quad part on the caller's stream, lane part on a
-//        CU-masked stream -- a CU-masked stream gets a hardware queue of its
-//        own instead of one of the process's GPU_MAX_HW_QUEUES shared ones,
-//        so the lane part can never queue behind the quad part;
-//   own2: both parts on CU-masked streams of their own;
+// a device first orders a batch; A/B in tools/queue_probe.py,
+// profiles/r02/queue_probe_*.log):
+//   hiq (default): quad part on a non-blocking stream of the greatest
+//        priority, lane part on the caller's stream.  HIP pools hardware
+//        queues per priority, so the quad part never shares a queue with the
+//        caller's (or any other normal-priority) stream, and its workgroups
+//        are dispatched first;
+//   own2: both parts on CU-masked streams (a hardware queue each; these are
+//        blocking streams, so they synchronise with the null stream);
 //   plain: quad part on the caller's stream, lane part on a plain stream
 //        (round 1: the two serialised whenever they shared a queue).
-enum PartMode { kPartOwn1 = 0, kPartOwn2 = 1, kPartPlain = 2 };
+enum PartMode { kPartHiq = 0, kPartOwn2 = 1, kPartPlain = 2 };
 static int part_mode() {
   const char* v = std::getenv("CIR_PART_STREAMS");
   if (v && strcmp(v, "own2") == 0) return kPartOwn2;
   if (v && strcmp(v, "plain") == 0) return kPartPlain;
-  return kPartOwn1;
+  return kPartHiq;
 }
 
-static hipError_t create_part_stream(int dev_id, bool own_queue, hipStream_t* s) {
-  if (!own_queue) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+static hipError_t create_cu_masked_stream(int dev_id, hipStream_t* s) {
   hipDeviceProp_t prop;
   hipError_t e = hipGetDeviceProperties(&prop, dev_id);
   if (e != hipSuccess) return e;
   std::vector<uint32_t> mask((prop.multiProcessorCount + 31) / 32, 0u);
   for (int c = 0; c < prop.multiProcessorCount; ++c) mask[c / 32] |= 1u << (c % 32);
   return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
+}
+
+static hipError_t create_part_streams(Device& d) {
+  d.part_mode = part_mode();
+  if (d.part_mode == kPartOwn2) {
+    hipError_t e = create_cu_masked_stream(d.id, &d.qstream);
+    return e != hipSuccess ? e : create_cu_masked_stream(d.id, &d.aux);
+  }
+  if (d.part_mode == kPartPlain) return hipStreamCreateWithFlags(&d.aux, hipStreamNonBlocking);
+  int least = 0, greatest = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+  if (e != hipSuccess) return e;
+  return hipStreamCreateWithPriority(&d.qstream, hipStreamNonBlocking, greatest);
 }
 
 // Descriptor batch, longest chain first: device sort (order.hip) into the
@@ -172,9 +187,7 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
   const size_t need = dev::order_scratch_bytes(n);
   if (!d.order_free) {
     CIR_HIP(hipEventCreateWithFlags(&d.order_free, hipEventDisableTiming));
-    d.part_mode = part_mode();
-    if (d.part_mode == kPartOwn2) CIR_HIP(create_part_stream(d.id, true, &d.qstream));
-    CIR_HIP(create_part_stream(d.id, d.part_mode != kPartPlain, &d.aux));
+    CIR_HIP(create_part_streams(d));
     CIR_HIP(hipEventCreateWithFlags(&d.aux_fork, hipEventDisableTiming));
     CIR_HIP(hipEventCreateWithFlags(&d.aux_join, hipEventDisableTiming));
     CIR_HIP(hipEventCreateWithFlags(&d.q_join, hipEventDisableTiming));
@@ -194,8 +207,8 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
   if (ht == CIR_HASH_SHA512_256)
     CIR_HIP(dev::launch_sha_desc(arena, off, len, perm, n, out, s));
   else
-    CIR_HIP(dev::launch_mixed(arena, off, len, perm, n_long, n, out, s,
-                              d.qstream ? d.qstream : s, d.aux, d.aux_fork, d.q_join, d.aux_join));
+    CIR_HIP(dev::launch_mixed(arena, off, len, perm, n_long, n, out, s, d.qstream ? d.qstream : s,
+                              d.aux ? d.aux : s, d.aux_fork, d.q_join, d.aux_join));
   CIR_HIP(hipEventRecord(d.order_free, s));
   return CIR_OK;
 }

@@ -82,12 +82,10 @@ struct Device {
   void* order_scratch = nullptr;
   size_t order_cap = 0;
   hipEvent_t order_free = nullptr;
-  // An ordered batch runs its lane part on `aux` (and, in part mode own2,
-  // its quad part on `qstream`; otherwise on the caller's stream), forked
-  // from and joined back into the caller's stream with events.  aux is
-  // CU-masked, which gives it a hardware queue of its own: the two parts run
-  // concurrently whatever queue the caller's stream shares (runtime.cpp
-  // part_mode).
+  // An ordered batch runs its quad part on `qstream` (a high-priority
+  // stream: a hardware queue of its own) and its lane part on the caller's
+  // stream, forked and joined with events (runtime.cpp part_mode; a null
+  // qstream / aux means the caller's stream).
   int part_mode = 0;
   hipStream_t aux = nullptr, qstream = nullptr;
   hipEvent_t aux_fork = nullptr, aux_join = nullptr, q_join = nullptr;
