@@ -281,14 +281,16 @@ __device__ __forceinline__ void quad_chains(const uint8_t* __restrict__ arena,
   quad_chain<kPrefetchAll, kAsm>(have, b, arena + o, L, out, lds, wave_lds);
 }
 
-// Hashes::hash_file split of one device-resident file with fewer than
-// kQuadSmallBatch blocks: every block in quad mode (16 per wave).
+// Hashes::hash_file split of one device-resident file, blocks [b0, nblk):
+// every block in quad mode (16 per wave).  The whole file when it has fewer
+// than kQuadSmallBatch blocks; otherwise the ragged rest beside k_chunks'
+// uniform part (launch_chunks_split).
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_quad_chunks(
-    const uint8_t* __restrict__ data, uint64_t nbytes, uint64_t bs, uint64_t nblk,
+    const uint8_t* __restrict__ data, uint64_t nbytes, uint64_t bs, uint64_t b0, uint64_t nblk,
     uint8_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWaves * kQuadWaveLds];
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t first = ((uint64_t)blockIdx.x * kWaves + wave) * 16u;
+  const uint64_t first = b0 + ((uint64_t)blockIdx.x * kWaves + wave) * 16u;
   if (first >= nblk) return;
   __builtin_amdgcn_s_setprio(3);
   const uint64_t b = first + ((threadIdx.x & 63u) >> 2);
@@ -541,7 +543,7 @@ hipError_t launch_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint
   const uint64_t nblk = (nbytes + bs - 1) / bs;
   if (nblk < kQuadSmallBatch && bs >= 128ull * kQuadSmallMinLines && bs <= 0xffffffffull) {
     hipLaunchKernelGGL(k_quad_chunks, dim3((unsigned)((nblk + 63) / 64)), dim3(kThreads), 0, s,
-                       data, nbytes, bs, nblk, out);
+                       data, nbytes, bs, (uint64_t)0, nblk, out);
     return hipGetLastError();
   }
   const bool uni_ok = bs % 128u == 0 && (reinterpret_cast<uintptr_t>(data) & 15u) == 0 &&
@@ -555,6 +557,41 @@ hipError_t launch_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint
   hipLaunchKernelGGL(k_chunks, dim3((unsigned)grid), dim3(kThreads), 0, s, data, nbytes, bs,
                      (uint32_t)(bs / 128u), nuni, nblk, (uint32_t)ngen_wg, out);
   return hipGetLastError();
+}
+
+// launch_chunks with the ragged rest (fewer than 256 whole blocks plus the
+// short last block) hashed in quad mode on qs, concurrently with the uniform
+// part on s.  In lane mode the rest's chains have no line prefetch and ran
+// ~15-25 % longer than the uniform waves, trailing the launch (65535 x 32 KiB
+// at 1334 GiB/s against 1548 at 65536, profiles/r01/shapes.log); in quad mode
+// a chain takes about a third of a lane-mode chain's time.  Forked from s
+// (`fork`), joined back (`join`).  Falls back to launch_chunks where the
+// split does not apply.
+hipError_t launch_chunks_split(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint8_t* out,
+                               hipStream_t s, hipStream_t qs, hipEvent_t fork, hipEvent_t join) {
+  if (nbytes == 0) return hipSuccess;
+  if (bs == 0) return hipErrorInvalidValue;
+  const uint64_t nblk = (nbytes + bs - 1) / bs;
+  const bool uni_ok = bs % 128u == 0 && (reinterpret_cast<uintptr_t>(data) & 15u) == 0 &&
+                      bs / 128u <= 0xffffffffull && bs <= 0xffffffffull / 8u;
+  const uint64_t nuni = (nbytes / bs) / kThreads * kThreads;
+  if (!qs || qs == s || nblk < kQuadSmallBatch || !uni_ok || nuni == nblk ||
+      bs < 128ull * kQuadSmallMinLines || nuni / kThreads > 0x7fffffffull)
+    return launch_chunks(data, nbytes, bs, out, s);
+  hipError_t e = hipEventRecord(fork, s);
+  if (e == hipSuccess) e = hipStreamWaitEvent(qs, fork, 0);
+  if (e != hipSuccess) return e;
+  const uint64_t nrest = nblk - nuni;
+  hipLaunchKernelGGL(k_quad_chunks, dim3((unsigned)((nrest + 63) / 64)), dim3(kThreads), 0, qs,
+                     data, nbytes, bs, nuni, nblk, out);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_chunks, dim3((unsigned)(nuni / kThreads)), dim3(kThreads), 0, s, data,
+                     nbytes, bs, (uint32_t)(bs / 128u), nuni, nuni, 0u, out);
+  e = hipGetLastError();
+  if (e == hipSuccess) e = hipEventRecord(join, qs);
+  if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
+  return e;
 }
 
 hipError_t launch_general_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs,

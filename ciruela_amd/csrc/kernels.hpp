@@ -52,6 +52,12 @@ hipError_t launch_uniform(Loader loader, const uint8_t* data, uint64_t bs, uint6
 hipError_t launch_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint8_t* out,
                          hipStream_t s);
 
+// launch_chunks with the ragged rest in quad mode on qs, concurrently with
+// the uniform part on s (fork / join events); launch_chunks where that does
+// not apply (small or misaligned files, no rest, qs null or == s).
+hipError_t launch_chunks_split(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint8_t* out,
+                               hipStream_t s, hipStream_t qs, hipEvent_t fork, hipEvent_t join);
+
 // Blocks first .. first+n-1 of Hashes::hash_file's split of [data, data+nbytes).
 hipError_t launch_general_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs,
                                  uint64_t first, uint64_t n, uint8_t* out, hipStream_t s);

@@ -168,6 +168,28 @@ static hipError_t create_part_streams(Device& d) {
   return hipStreamCreateWithPriority(&d.qstream, hipStreamNonBlocking, greatest);
 }
 
+// The part streams and their events, created on first use (caller holds
+// d.order_mu with d's device current).
+int ensure_part_streams(Device& d) {
+  if (d.order_free) return CIR_OK;
+  CIR_HIP(create_part_streams(d));
+  CIR_HIP(hipEventCreateWithFlags(&d.aux_fork, hipEventDisableTiming));
+  CIR_HIP(hipEventCreateWithFlags(&d.aux_join, hipEventDisableTiming));
+  CIR_HIP(hipEventCreateWithFlags(&d.q_join, hipEventDisableTiming));
+  CIR_HIP(hipEventCreateWithFlags(&d.order_free, hipEventDisableTiming));
+  return CIR_OK;
+}
+
+// The context's state of the device `s` belongs to (NULL: the calling
+// thread's current device), or null if the context does not hold it.
+Device* stream_device(cir_ctx* ctx, hipStream_t s) {
+  int id = 0;
+  if ((s ? hipStreamGetDevice(s, &id) : hipGetDevice(&id)) != hipSuccess) return nullptr;
+  for (auto& p : ctx->devs)
+    if (p->id == id) return p.get();
+  return nullptr;
+}
+
 // Descriptor batch, longest chain first: device sort (order.hip) into the
 // device's ordering scratch, then the general kernel through the permutation.
 bool valid_hash_type(int ht) { return ht == CIR_HASH_BLAKE2B_256 || ht == CIR_HASH_SHA512_256; }
@@ -185,13 +207,8 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
   DeviceGuard guard;
   CIR_HIP(hipSetDevice(d.id));
   const size_t need = dev::order_scratch_bytes(n);
-  if (!d.order_free) {
-    CIR_HIP(hipEventCreateWithFlags(&d.order_free, hipEventDisableTiming));
-    CIR_HIP(create_part_streams(d));
-    CIR_HIP(hipEventCreateWithFlags(&d.aux_fork, hipEventDisableTiming));
-    CIR_HIP(hipEventCreateWithFlags(&d.aux_join, hipEventDisableTiming));
-    CIR_HIP(hipEventCreateWithFlags(&d.q_join, hipEventDisableTiming));
-  }
+  int rc = ensure_part_streams(d);
+  if (rc) return rc;
   if (need > d.order_cap) {
     CIR_HIP(hipEventSynchronize(d.order_free));
     (void)hipFree(d.order_scratch);
@@ -615,13 +632,25 @@ void cir_free(void* p) { free(p); }
 
 int cir_hash_chunks_dev(cir_ctx* ctx, const void* d_data, uint64_t nbytes, uint64_t block_size,
                         uint8_t* d_out, void* stream) {
-  (void)ctx;
   if (block_size == 0) return fail(CIR_EINVAL, "block_size must be > 0");
   if (nbytes && (!d_data || !d_out)) return fail(CIR_EINVAL, "null device pointer");
   if (reinterpret_cast<uintptr_t>(d_out) & 15u)
     return fail(CIR_EINVAL, "d_out must be 16-byte aligned");
-  CIR_HIP(dev::launch_chunks((const uint8_t*)d_data, nbytes, block_size, d_out,
-                             (hipStream_t)stream));
+  hipStream_t s = (hipStream_t)stream;
+  // with a context, the ragged rest of a large file runs in quad mode on the
+  // device's quad-part stream beside the uniform part (launch_chunks_split)
+  Device* d = ctx ? stream_device(ctx, s) : nullptr;
+  if (d && nbytes) {
+    std::lock_guard<std::mutex> lk(d->order_mu);
+    DeviceGuard guard;
+    CIR_HIP(hipSetDevice(d->id));
+    int rc = ensure_part_streams(*d);
+    if (rc) return rc;
+    CIR_HIP(dev::launch_chunks_split((const uint8_t*)d_data, nbytes, block_size, d_out, s,
+                                     d->qstream, d->aux_fork, d->q_join));
+    return CIR_OK;
+  }
+  CIR_HIP(dev::launch_chunks((const uint8_t*)d_data, nbytes, block_size, d_out, s));
   return CIR_OK;
 }
 
@@ -641,14 +670,7 @@ int cir_hash_blocks_dev_ht(cir_ctx* ctx, int hash_type, const void* d_arena,
   // context the batch is ordered longest chain first on the device
   // (order.hip) and long BLAKE2b chains run in quad mode.
   if (ctx) {
-    int id = 0;
-    if (s)
-      CIR_HIP(hipStreamGetDevice(s, &id));
-    else
-      CIR_HIP(hipGetDevice(&id));
-    Device* d = nullptr;
-    for (auto& p : ctx->devs)
-      if (p->id == id) d = p.get();
+    Device* d = stream_device(ctx, s);
     if (!d) return fail(CIR_EINVAL, "stream device is not part of the context");
     return hash_desc_ordered(*d, (const uint8_t*)d_arena, d_off, d_len, nblk, d_out, s, hash_type);
   }

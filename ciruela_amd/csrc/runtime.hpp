@@ -117,6 +117,7 @@ int slot_submit(Device& d, Slot& s, uint64_t bytes, uint64_t nblk, int ht = CIR_
 int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, const uint32_t* len,
                       uint64_t n, uint8_t* out, hipStream_t s, int ht = CIR_HASH_BLAKE2B_256);
 bool valid_hash_type(int ht);
+int ensure_part_streams(Device& d);
 int slot_wait(Device& d, Slot& s);
 
 }  // namespace cir
@@ -125,3 +126,7 @@ struct cir_ctx {
   std::vector<std::unique_ptr<cir::Device>> devs;
   uint64_t staging = 0;
 };
+
+namespace cir {
+Device* stream_device(cir_ctx* ctx, hipStream_t s);
+}  // namespace cir

@@ -114,6 +114,10 @@ def test_hash_bytes(gpu, oracle):
     (1000, 70000 * 1000 + 7),
     (128, 65536 * 128),
     (32768, 49152 * 32768 + 99),   # one block past the quad-mode batch limit
+    # with a context the ragged rest runs in quad mode beside the uniform
+    # part (launch_chunks_split): 255 whole blocks, and whole + short ones
+    (32768, 65535 * 32768),
+    (1024, 65535 * 1024 + 3),
 ])
 def test_chunks_dev_vs_oracle(gpu, ctx, oracle, bs, nbytes):
     import torch
@@ -810,3 +814,18 @@ def test_rewrite_rejects_invalid_paths(gpu, small_ctx):
         with pytest.raises(gpu.CiruelaError) as e:
             small_ctx.index_rewrite(idx)
         assert e.value.status == gpu._n.CIR_EPARSE
+
+
+@pytest.mark.parametrize("bs,nbytes", [(4096, 70000 * 4096 + 1234), (32768, 65535 * 32768)])
+def test_chunks_dev_without_context(gpu, oracle, bs, nbytes):
+    """cir_hash_chunks_dev with a NULL context: the fused single launch
+    (k_chunks with the ragged rest in lane mode) gives the same digests."""
+    import torch
+    data = dev_random(gpu, nbytes, seed=bs + nbytes)
+    nb = (nbytes + bs - 1) // bs
+    out = torch.zeros(nb * 32, dtype=torch.uint8, device="cuda:0")
+    gpu._n.check(gpu._n.lib.cir_hash_chunks_dev(None, data.data_ptr(), nbytes, bs,
+                                                out.data_ptr(), None))
+    torch.cuda.synchronize()
+    want = oracle_chunks(oracle, data.cpu().numpy(), nbytes, bs)
+    assert first_bad(out.cpu().numpy(), want) is None
