@@ -50,40 +50,41 @@ __global__ __launch_bounds__(kThreads, 5) void k_uniform_glds(const uint8_t* __r
   uniform_glds_wave(data + blk0 * bs, bs, lines, out + blk0 * 32u, lds + wave * kWaveLds);
 }
 
-// Hashes::hash_file over one device-resident file, fused in one launch:
-// workgroups [0, ngen_wg) hash the blocks nuni .. nblk-1 (the ragged rest:
-// fewer than 256 whole blocks plus the short last block) one lane per chain
-// with vector loads (hash_chain_al16: the file is 16-B aligned and bs % 128
-// == 0 whenever this kernel runs; misaligned files go to k_general), the
-// others hash blocks [0, nuni) 64 per wave through LDS.  The
-// ragged workgroups come first so their chains start with the rest instead
-// of trailing the launch.
+// Hashes::hash_file over one device-resident file (16-B aligned, bs % 128
+// == 0), fused in one launch: the whole blocks [0, nfull) 64 per wave
+// through LDS (workgroups ngen_wg.., the file's last wave possibly partial),
+// and when ngen_wg == 1 the short last block (block nfull) on one lane of
+// workgroup 0 with vector loads (hash_chain_al16).  With a context the short
+// block runs in quad mode on another stream instead (launch_chunks_split).
 // 4 waves per SIMD (128-VGPR budget): the uniform body needs 90 VGPRs, the
-// fused ragged branch ~100; at 5 (96 VGPRs) the ragged branch spilled 6
-// VGPRs to scratch.  4 and 5 waves run config 2 within 0.02 % of each other
-// (profiles/r01/ablib_nt_occ.log: 14.859 vs 14.857 ms): the body is
-// issue-bound, not latency-bound.
+// ragged branch ~100; at 5 (96 VGPRs) the ragged branch spilled 6 VGPRs to
+// scratch.  4 and 5 waves run config 2 within 0.2 % of each other
+// (profiles/r02/ablib_occ4_vs_occ5.log): the body is issue-bound.
 #ifndef CIR_UNI_OCC
 #define CIR_UNI_OCC 4
 #endif
 __global__ __launch_bounds__(kThreads, CIR_UNI_OCC) void k_chunks(const uint8_t* __restrict__ data,
                                                          uint64_t nbytes, uint64_t bs,
-                                                         uint32_t lines, uint64_t nuni,
-                                                         uint64_t nblk, uint32_t ngen_wg,
+                                                         uint32_t lines, uint64_t nfull,
+                                                         uint32_t ngen_wg,
                                                          uint8_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWaves * kWaveLds];
   if (blockIdx.x < ngen_wg) {
-    const uint64_t b = nuni + (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (b >= nblk) return;
-    const uint64_t o = b * bs, rest = nbytes - o;
+    if (threadIdx.x != 0) return;
     uint64_t h[8];
-    hash_chain_al16(data + o, rest < bs ? rest : bs, h);  // launched only 16-B aligned
-    store_digest(out + b * 32u, h);
+    hash_chain_al16(data + nfull * bs, nbytes - nfull * bs, h);  // launched only 16-B aligned
+    store_digest(out + nfull * 32u, h);
     return;
   }
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // scalar
   const uint64_t blk0 = ((uint64_t)(blockIdx.x - ngen_wg) * kWaves + wave) * 64u;
-  uniform_glds_wave(data + blk0 * bs, bs, lines, out + blk0 * 32u, lds + wave * kWaveLds);
+  if (blk0 >= nfull) return;
+  const uint64_t nv = nfull - blk0;
+  if (nv >= 64)
+    uniform_glds_wave(data + blk0 * bs, bs, lines, out + blk0 * 32u, lds + wave * kWaveLds);
+  else
+    uniform_glds_wave<true>(data + blk0 * bs, bs, lines, out + blk0 * 32u, lds + wave * kWaveLds,
+                            (uint32_t)nv);
 }
 
 __global__ __launch_bounds__(kThreads, 4) void k_uniform_direct(const uint8_t* __restrict__ data,
@@ -550,44 +551,42 @@ hipError_t launch_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint
                       bs / 128u <= 0xffffffffull && bs <= 0xffffffffull / 8u;
   if (!uni_ok)  // misaligned base or bs % 128 != 0: every block ragged
     return launch_general_chunks(data, nbytes, bs, 0, nblk, out, s);
-  const uint64_t nuni = (nbytes / bs) / kThreads * kThreads;
-  const uint64_t ngen_wg = grid_for(nblk - nuni, kThreads);
-  const uint64_t grid = ngen_wg + nuni / kThreads;
+  const uint64_t nfull = nbytes / bs;
+  const uint32_t ngen_wg = nfull < nblk ? 1u : 0u;  // the short last block
+  const uint64_t grid = ngen_wg + grid_for(grid_for(nfull, 64), kWaves);
   if (grid > 0x7fffffffull) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_chunks, dim3((unsigned)grid), dim3(kThreads), 0, s, data, nbytes, bs,
-                     (uint32_t)(bs / 128u), nuni, nblk, (uint32_t)ngen_wg, out);
+                     (uint32_t)(bs / 128u), nfull, ngen_wg, out);
   return hipGetLastError();
 }
 
-// launch_chunks with the ragged rest (fewer than 256 whole blocks plus the
-// short last block) hashed in quad mode on qs, concurrently with the uniform
-// part on s.  In lane mode the rest's chains have no line prefetch and ran
-// ~15-25 % longer than the uniform waves, trailing the launch (65535 x 32 KiB
-// at 1334 GiB/s against 1548 at 65536, profiles/r01/shapes.log); in quad mode
-// a chain takes about a third of a lane-mode chain's time.  Forked from s
-// (`fork`), joined back (`join`).  Falls back to launch_chunks where the
-// split does not apply.
+// launch_chunks with the short last block hashed in quad mode on qs,
+// concurrently with the whole blocks on s.  One lane-mode chain of up to bs
+// bytes without line prefetch runs ~25-35 % longer than a uniform wave's
+// chains and trailed the launch; in quad mode it takes about a third of a
+// lane-mode chain's time.  Forked from s (`fork`), joined back (`join`).
+// Falls back to launch_chunks where the split does not apply.
 hipError_t launch_chunks_split(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint8_t* out,
                                hipStream_t s, hipStream_t qs, hipEvent_t fork, hipEvent_t join) {
   if (nbytes == 0) return hipSuccess;
   if (bs == 0) return hipErrorInvalidValue;
   const uint64_t nblk = (nbytes + bs - 1) / bs;
+  const uint64_t nfull = nbytes / bs;
   const bool uni_ok = bs % 128u == 0 && (reinterpret_cast<uintptr_t>(data) & 15u) == 0 &&
                       bs / 128u <= 0xffffffffull && bs <= 0xffffffffull / 8u;
-  const uint64_t nuni = (nbytes / bs) / kThreads * kThreads;
-  if (!qs || qs == s || nblk < kQuadSmallBatch || !uni_ok || nuni == nblk ||
-      bs < 128ull * kQuadSmallMinLines || nuni / kThreads > 0x7fffffffull)
+  const uint64_t grid = grid_for(grid_for(nfull, 64), kWaves);
+  if (!qs || qs == s || nblk < kQuadSmallBatch || !uni_ok || nfull == nblk ||
+      bs < 128ull * kQuadSmallMinLines || grid > 0x7fffffffull)
     return launch_chunks(data, nbytes, bs, out, s);
   hipError_t e = hipEventRecord(fork, s);
   if (e == hipSuccess) e = hipStreamWaitEvent(qs, fork, 0);
   if (e != hipSuccess) return e;
-  const uint64_t nrest = nblk - nuni;
-  hipLaunchKernelGGL(k_quad_chunks, dim3((unsigned)((nrest + 63) / 64)), dim3(kThreads), 0, qs,
-                     data, nbytes, bs, nuni, nblk, out);
+  hipLaunchKernelGGL(k_quad_chunks, dim3(1), dim3(kThreads), 0, qs, data, nbytes, bs, nfull, nblk,
+                     out);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_chunks, dim3((unsigned)(nuni / kThreads)), dim3(kThreads), 0, s, data,
-                     nbytes, bs, (uint32_t)(bs / 128u), nuni, nuni, 0u, out);
+  hipLaunchKernelGGL(k_chunks, dim3((unsigned)grid), dim3(kThreads), 0, s, data, nbytes, bs,
+                     (uint32_t)(bs / 128u), nfull, 0u, out);
   e = hipGetLastError();
   if (e == hipSuccess) e = hipEventRecord(join, qs);
   if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);

@@ -35,9 +35,17 @@ constexpr int kWaveLds = 8192;
 // The per-lane DMA offsets and LDS read addresses are recomputed every line
 // from one register each (one full-rate v_xor_b32 apiece) instead of being
 // hoisted into 16 + 8 registers; the DMA base address stays scalar.
+//
+// kPartial: the wave's last block is wsrc block nv - 1 (nv < 64, the file's
+// last whole blocks): the DMA rows of blocks >= nv re-read block nv - 1 (in
+// bounds; their lanes hash a duplicate) and only lanes < nv store.  A file
+// whose whole-block count is not a multiple of 64 then still hashes every
+// whole block through the prefetching LDS-DMA body instead of the slower
+// general loader.
+template <bool kPartial = false>
 __device__ __forceinline__ void uniform_glds_wave(const uint8_t* __restrict__ wsrc, uint64_t bs,
                                                   uint32_t lines, uint8_t* __restrict__ out,
-                                                  uint8_t* wl) {
+                                                  uint8_t* wl, uint32_t nv = 64) {
   const uint32_t lane = threadIdx.x & 63u;
   // DMA lane offset: r*bs + 16*chunk, chunk = (l & 7) ^ r ^ j
   const uint32_t r = lane >> 3;
@@ -51,7 +59,13 @@ __device__ __forceinline__ void uniform_glds_wave(const uint8_t* __restrict__ ws
     const uint8_t* line = wsrc + (uint64_t)i * 128u;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const uint8_t* src = line + (uint64_t)j * jstride + (dma_lane ^ (16u * j));
+      const uint8_t* src;
+      if constexpr (kPartial) {
+        const uint32_t blk = min(8u * j + r, nv - 1u);
+        src = line + (uint64_t)blk * bs + ((16u * ((lane & 7u) ^ r)) ^ (16u * j));
+      } else {
+        src = line + (uint64_t)j * jstride + (dma_lane ^ (16u * j));
+      }
       __builtin_amdgcn_global_load_lds(
           (const void __attribute__((address_space(1)))*)src,
           (void __attribute__((address_space(3)))*)(wl + j * 1024), 16, 0, CIR_DMA_AUX);
@@ -77,7 +91,7 @@ __device__ __forceinline__ void uniform_glds_wave(const uint8_t* __restrict__ ws
     const bool last = i + 1 == lines;
     compress(h, m, (uint64_t)(i + 1) * 128u, last);
   }
-  store_digest(out + lane * 32u, h);
+  if (!kPartial || lane < nv) store_digest(out + lane * 32u, h);
 }
 
 }  // namespace dev

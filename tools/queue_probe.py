@@ -5,8 +5,9 @@ its first ordered batch the quad-part / lane-part streams).  With
 GPU_MAX_HW_QUEUES = 4 (HIP's default) ordinary streams of a process share
 hardware queues, and when the quad and lane parts of a mixed batch landed on
 one queue they ran one after the other (r01: 570-610 GiB/s instead of ~850).
-CIR_PART_STREAMS = own1 (default: lane part on a CU-masked stream, i.e. a
-queue of its own) / own2 (both parts on CU-masked streams) / plain (round 1).
+CIR_PART_STREAMS = hiq (default: quad part on a high-priority stream, a
+queue pool of its own) / own2 (both parts on CU-masked streams) / plain
+(round 1).
 
     python tools/queue_probe.py --contexts 4 [--steps 10]
 """
@@ -60,7 +61,7 @@ def main():
     dt = (time.perf_counter() - t0) / args.steps
     hashed = int(lens.astype("int64").sum())
     print("config3 contexts=%d part_streams=%s: %.3f ms  %.1f GiB/s" % (
-        args.contexts, os.environ.get("CIR_PART_STREAMS", "own1"), dt * 1e3,
+        args.contexts, os.environ.get("CIR_PART_STREAMS", "hiq"), dt * 1e3,
         hashed / dt / (1 << 30)), flush=True)
 
 
