@@ -26,6 +26,7 @@
 #include "kernels.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "blake2b_dev.hpp"
 #include "uniform.hpp"
@@ -321,6 +322,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))
   if (first >= nl) return;
   __builtin_amdgcn_s_setprio(3);
   quad_chains<true, kAsm>(arena, off, len, perm, first, nl, out, lds, wave * kQuadWaveLds);
+}
+
+// How long the lane part waits for the quad part's workgroups to take their
+// CUs: k_delay rounds (CIR_QUAD_LEAD_ROUNDS, default 6 = ~20 us).
+static uint32_t quad_lead_rounds() {
+  static const uint32_t r = [] {
+    const char* v = std::getenv("CIR_QUAD_LEAD_ROUNDS");
+    return v && *v ? (uint32_t)std::atoi(v) : 6u;
+  }();
+  return r;
 }
 
 // A bounded pause on a stream: `rounds` x s_sleep 127 (~3.4 us each).
@@ -631,7 +642,7 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
                        arena, off, len, perm, n_long, (uint32_t)nq, out);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, aux, 6u);
+    hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, aux, quad_lead_rounds());
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads), 0, aux, arena, off,
