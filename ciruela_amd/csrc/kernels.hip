@@ -312,10 +312,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))
 template <bool kAsm, bool kExclusive>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_quad_long(
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ off,
-    const uint32_t* __restrict__ len, const uint32_t* __restrict__ perm, const uint32_t* n_long,
+    const uint32_t* __restrict__ len, const uint32_t* __restrict__ perm, uint32_t* n_long,
     uint32_t nq_wg, uint8_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWaves * kQuadWaveLds];
-  if constexpr (kExclusive) asm volatile("v_accvgpr_write_b32 a255, 0" ::: "a255");
+  if constexpr (kExclusive) {
+    asm volatile("v_accvgpr_write_b32 a255, 0" ::: "a255");
+    // this workgroup holds its CU: count it for k_gate (n_long[1])
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(n_long + 1, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+  }
   const uint32_t nl = min(*n_long, nq_wg * 64u);
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t first = (blockIdx.x * kWaves + wave) * 16u;
@@ -324,19 +329,20 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))
   quad_chains<true, kAsm>(arena, off, len, perm, first, nl, out, lds, wave * kQuadWaveLds);
 }
 
-// How long the lane part waits for the quad part's workgroups to take their
-// CUs: k_delay rounds (CIR_QUAD_LEAD_ROUNDS, default 6 = ~20 us).
-static uint32_t quad_lead_rounds() {
-  static const uint32_t r = [] {
-    const char* v = std::getenv("CIR_QUAD_LEAD_ROUNDS");
-    return v && *v ? (uint32_t)std::atoi(v) : 6u;
-  }();
-  return r;
-}
-
-// A bounded pause on a stream: `rounds` x s_sleep 127 (~3.4 us each).
-__global__ void k_delay(uint32_t rounds) {
-  for (uint32_t r = 0; r < rounds; ++r) __builtin_amdgcn_s_sleep(127);
+// The lane part of an exclusive mixed batch waits until every quad
+// workgroup holds its CU (so lane waves cannot take the CUs the quad part
+// needs whole): one wave polls the quad part's started-workgroup counter,
+// sleeping ~3.4 us between polls, for at most max_rounds polls (~2 ms; the
+// gate never waits on anything else, so it cannot deadlock: if the quad part
+// is held up by other work, the lane part just starts after the bound).
+// Round 1 waited a fixed ~20 us (k_delay): with several contexts' streams in
+// one process the quad part's dispatch lagged behind that and config 3 lost
+// 12 % (profiles/r02/queue_probe_v2_hiq.log, lead.log).
+__global__ void k_gate(const uint32_t* started, uint32_t target, uint32_t max_rounds) {
+  for (uint32_t r = 0; r < max_rounds; ++r) {
+    if (__hip_atomic_load(started, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return;
+    __builtin_amdgcn_s_sleep(127);
+  }
 }
 
 // Lane part: chains [nl, n) of the order, one lane per chain.
@@ -622,7 +628,7 @@ hipError_t launch_general_desc(const uint8_t* arena, const uint64_t* off, const 
 }
 
 hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
-                        const uint32_t* perm, const uint32_t* n_long, uint64_t n, uint8_t* out,
+                        const uint32_t* perm, uint32_t* n_long, uint64_t n, uint8_t* out,
                         hipStream_t s, hipStream_t qs, hipStream_t aux, hipEvent_t fork,
                         hipEvent_t qjoin, hipEvent_t ljoin) {
   if (n == 0) return hipSuccess;
@@ -636,13 +642,14 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
   if (e != hipSuccess) return e;
   if (exclusive) {
     // The quad workgroups need whole CUs (one 504-register wave per SIMD):
-    // they are dispatched first, and the lane part starts ~20 us later, so
-    // its waves fill the other CUs instead of taking every SIMD first.
+    // they are dispatched first, and the lane part starts once all of them
+    // hold their CUs (k_gate), so its waves fill the other CUs instead of
+    // taking every SIMD first.
     hipLaunchKernelGGL((k_quad_long<kQuadAsm, true>), dim3((unsigned)nq), dim3(kThreads), 0, qs,
                        arena, off, len, perm, n_long, (uint32_t)nq, out);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, aux, quad_lead_rounds());
+    hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, aux, n_long + 1, (uint32_t)nq, 600u);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads), 0, aux, arena, off,

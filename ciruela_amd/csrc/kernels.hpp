@@ -72,14 +72,15 @@ hipError_t launch_general_desc(const uint8_t* arena, const uint64_t* off, const 
 // qs, the rest one lane per chain on `aux`; both fork from s (`fork`) and
 // join back into s (`qjoin`, `ljoin`).
 hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
-                        const uint32_t* perm, const uint32_t* n_long, uint64_t n, uint8_t* out,
+                        const uint32_t* perm, uint32_t* n_long, uint64_t n, uint8_t* out,
                         hipStream_t s, hipStream_t qs, hipStream_t aux, hipEvent_t fork,
                         hipEvent_t qjoin, hipEvent_t ljoin);
 
 // Longest-chain-first order of a descriptor batch (order.hip): *perm points
 // into `scratch` (order_scratch_bytes(n) bytes, device memory).
 size_t order_scratch_bytes(uint64_t n);
-// *n_long = number of chains with >= quad_min_lines(n) lines (device memory).
+// *n_long = number of chains with >= quad_min_lines(n) lines (device memory);
+// (*n_long)[1] = 0, the started-workgroup counter of the quad part.
 hipError_t launch_order_desc(const uint32_t* len, uint64_t n, void* scratch, size_t bytes,
                              uint32_t** perm, uint32_t** n_long, hipStream_t s);
 

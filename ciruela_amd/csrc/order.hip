@@ -38,7 +38,8 @@ hipError_t launch_order_desc(const uint32_t* len, uint64_t n, void* scratch, siz
   uint32_t* count = static_cast<uint32_t*>(scratch);
   uint8_t* p = static_cast<uint8_t*>(scratch) + 256;
   bytes -= 256;
-  hipError_t e0 = hipMemsetAsync(count, 0, 4, s);
+  // count[0] = n_long; count[1] = quad workgroups started (launch_mixed's gate)
+  hipError_t e0 = hipMemsetAsync(count, 0, 8, s);
   if (e0 != hipSuccess) return e0;
   *n_long = count;
   uint32_t* key_in = reinterpret_cast<uint32_t*>(p);
