@@ -4,7 +4,7 @@
 // Sorting descriptors by compression count (descending) puts chains of equal
 // length in the same waves and dispatches the longest ones first, so they
 // overlap with the short ones instead of trailing the launch.  The sort runs
-// on the device (hipCUB radix sort on 26-bit keys) inside the timed call.
+// on the device (hipCUB radix sort on 16-bit keys) inside the timed call.
 #include <hipcub/hipcub.hpp>
 
 #include "kernels.hpp"
@@ -12,23 +12,32 @@
 namespace cir {
 namespace dev {
 
+constexpr int kKeyBits = 16;  // k_chain_keys' key width
+
 __global__ void k_chain_keys(const uint32_t* __restrict__ len, uint64_t n, uint32_t min_lines,
-                             uint32_t* __restrict__ key, uint32_t* __restrict__ idx,
+                             uint16_t* __restrict__ key, uint32_t* __restrict__ idx,
                              uint32_t* __restrict__ n_long) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t l = len[i];
   const uint32_t k = l == 0 ? 1u : (l >> 7) + ((l & 127u) != 0);  // compressions, <= 2^25
-  key[i] = k;
+  // 16-bit sort key, monotone in k: exact below 32768 lines (4 MiB), then
+  // steps of 1024 lines (128 KiB) up to 2^25 lines.  With 2-byte keys
+  // rocPRIM sorts batches above 100 K items by onesweep (~4 launches); with
+  // 4-byte keys it chose block sort + merge sort up to 1 M items (~21
+  // launches).  The launches, not the work, dominate the ordering: ~7 us
+  // each, ~45 us each with several contexts' queues in one process
+  // (profiles/r02/gtrace*).
+  key[i] = (uint16_t)(k < 32768u ? k : 32768u + ((k - 32768u) >> 10));
   idx[i] = (uint32_t)i;
   if (k >= min_lines) atomicAdd(n_long, 1u);
 }
 
 size_t order_scratch_bytes(uint64_t n) {
   size_t temp = 0;
-  (void)hipcub::DeviceRadixSort::SortPairsDescending(nullptr, temp, (const uint32_t*)nullptr,
-                                                     (uint32_t*)nullptr, (const uint32_t*)nullptr,
-                                                     (uint32_t*)nullptr, (int)n, 0, 26);
+  (void)hipcub::DeviceRadixSort::SortPairsDescending(nullptr, temp, (const uint16_t*)nullptr,
+                                                     (uint16_t*)nullptr, (const uint32_t*)nullptr,
+                                                     (uint32_t*)nullptr, (int)n, 0, kKeyBits);
   return 256 + ((temp + 255) & ~(size_t)255) + 4 * ((n * 4 + 255) & ~(uint64_t)255);
 }
 
@@ -42,8 +51,8 @@ hipError_t launch_order_desc(const uint32_t* len, uint64_t n, void* scratch, siz
   hipError_t e0 = hipMemsetAsync(count, 0, 8, s);
   if (e0 != hipSuccess) return e0;
   *n_long = count;
-  uint32_t* key_in = reinterpret_cast<uint32_t*>(p);
-  uint32_t* key_out = reinterpret_cast<uint32_t*>(p + arr);
+  uint16_t* key_in = reinterpret_cast<uint16_t*>(p);
+  uint16_t* key_out = reinterpret_cast<uint16_t*>(p + arr);
   uint32_t* idx_in = reinterpret_cast<uint32_t*>(p + 2 * arr);
   uint32_t* idx_out = reinterpret_cast<uint32_t*>(p + 3 * arr);
   void* temp = p + 4 * arr;
@@ -57,7 +66,7 @@ hipError_t launch_order_desc(const uint32_t* len, uint64_t n, void* scratch, siz
     return hipSuccess;
   }
   e = hipcub::DeviceRadixSort::SortPairsDescending(temp, temp_bytes, key_in, key_out, idx_in,
-                                                   idx_out, (int)n, 0, 26, s);
+                                                   idx_out, (int)n, 0, kKeyBits, s);
   *perm = idx_out;
   return e;
 }
