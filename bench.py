@@ -342,7 +342,7 @@ def run_config2host(args, ca, ctx, dev, stream):
     = Hashes::hash_file over an in-memory file, digests back in host memory.
     The PCIe-inclusive rate of the headline shape; never `value`
     of the headline line."""
-    import numpy as np
+    import numpy as np  # noqa: F811
     import torch
     bs = args.block_size
     nbytes = args.host_gib << 30
@@ -363,11 +363,29 @@ def run_config2host(args, ca, ctx, dev, stream):
         got = ctx.hash_memory(host, bs)
         times.append(time.perf_counter() - t0)
     best = min(times)
+    # oracle check + CPU baseline on the same host buffer: its first 4 GiB
+    # (all special blocks included), Hashes::hash_file over memory on the CPU
+    lib = load_oracle()
+    sample = min(nbytes, 4 << 30)
+    want_cpu = np.empty(sample // bs * 32, dtype=np.uint8)
+
+    def run(threads):
+        lib.oracle_hash_chunks(host.ctypes.data, sample, bs, want_cpu.ctypes.data, threads)
+        return sample
+    rates = cpu_rates(run, args.cpu_seconds)
     return {"metric": "GiB/s block-hashed from host memory, config 2 shape (PCIe-inclusive)",
             "value": round(nbytes / best / GIB, 3), "unit": "GiB/s",
             "seconds_best": round(best, 3), "seconds_all": [round(t, 3) for t in times],
+            "config": {"workload": "config2host: %d x %d B blocks in a pageable host buffer "
+                                   "(%.0f GiB), cir_hash_memory" % (nbytes // bs, bs, nbytes / GIB)},
             "bytes": nbytes, "block_size": bs, "entry_point": "cir_hash_memory",
             "matches_device_resident": got == want,
+            "matches_oracle": got[:len(want_cpu)] == want_cpu.tobytes(),
+            "oracle_checked_blocks": sample // bs,
+            "cpu_baseline": cpu_record(rates, "the buffer's first %.0f GiB (%d blocks), "
+                                       "oracle_hash_chunks (Hashes::hash_file over memory); 4 "
+                                       "threads = reference default --disk-threads"
+                                       % (sample / GIB, sample // bs)),
             "note": "pageable host buffer -> pinned staging (16 copy threads) -> H2D -> "
                     "k_chunks -> D2H digests, double-buffered"}
 
@@ -396,13 +414,35 @@ def run_config2sha(args, ca, ctx, dev, stream):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
     import hashlib
+    import numpy as np
     ok = all(out[32 * i:32 * i + 32].cpu().numpy().tobytes() ==
              hashlib.new("sha512_256", data[i * bs:(i + 1) * bs].cpu().numpy().tobytes()).digest()
              for i in (0, 20, nblk - 1))
+    # oracle check + CPU baseline: the first 1 GiB of the arena (special
+    # blocks included) through the threaded SHA-512/256 oracle
+    lib = load_oracle()
+    lib.oracle_sha_chunks.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                      ctypes.c_void_p, ctypes.c_int]
+    sample = min(nblk, 32768) * bs
+    host = data[:sample].cpu().numpy()
+    got = out[:sample // bs * 32].cpu().numpy()
+    want = np.empty(sample // bs * 32, dtype=np.uint8)
+
+    def run(threads):
+        lib.oracle_sha_chunks(host.ctypes.data, sample, bs, want.ctypes.data, threads)
+        return sample
+    rates = cpu_rates(run, args.cpu_seconds)
     return {"metric": "GiB/s SHA-512/256 block-hashed, config 2 shape (device-resident)",
             "value": round(nblk * bs / dt / GIB, 3), "unit": "GiB/s",
             "ms_per_step": round(dt * 1e3, 3), "steps": args.steps, "blocks": nblk,
-            "block_size": bs, "spot_check_vs_hashlib": ok}
+            "config": {"workload": "config2sha: %d x %d B splitmix64 blocks as SHA-512/256 "
+                                   "descriptors, device-resident" % (nblk, bs)},
+            "block_size": bs, "spot_check_vs_hashlib": ok,
+            "matches_oracle": bool(np.array_equal(got, want)),
+            "oracle_checked_blocks": sample // bs,
+            "cpu_baseline": cpu_record(rates, "the first %d blocks (%.0f GiB), oracle_sha_chunks "
+                                       "(SHA-512/256); 4 threads = reference default "
+                                       "--disk-threads" % (sample // bs, sample / GIB))}
 
 
 def make_tree(root, gib, file_mib=32, ndirs=40, seed=0x5EED0005):

@@ -126,7 +126,10 @@ int oracle_blake2b256(uint8_t out[32], const uint8_t* in, size_t inlen) {
 /* ---- batch forms, threaded (CPU baseline: dir-signature hashes on a CPU
  *      pool of `threads` workers; here the unit of work is a block) ---- */
 
+int oracle_sha512_256(uint8_t out[32], const uint8_t* in, size_t inlen);
+
 struct job {
+  int sha; /* 1: SHA-512/256 (dir-signature HashType::sha512_256) */
   const uint8_t* arena;
   const uint64_t* off;
   const uint32_t* len;
@@ -147,13 +150,20 @@ static void* worker(void* arg) {
     if (b0 >= j->n) return NULL;
     size_t b1 = b0 + 64 < j->n ? b0 + 64 : j->n;
     for (size_t b = b0; b < b1; ++b) {
+      const uint8_t* p;
+      uint64_t l;
       if (j->off) {
-        oracle_blake2b256(j->out + 32 * b, j->arena + j->off[b], j->len[b]);
+        p = j->arena + j->off[b];
+        l = j->len[b];
       } else {
         uint64_t o = (uint64_t)b * j->bs;
-        uint64_t l = j->nbytes - o < j->bs ? j->nbytes - o : j->bs;
-        oracle_blake2b256(j->out + 32 * b, j->arena + o, l);
+        p = j->arena + o;
+        l = j->nbytes - o < j->bs ? j->nbytes - o : j->bs;
       }
+      if (j->sha)
+        oracle_sha512_256(j->out + 32 * b, p, l);
+      else
+        oracle_blake2b256(j->out + 32 * b, p, l);
     }
   }
 }
@@ -192,6 +202,21 @@ int oracle_hash_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint8_
   if (bs == 0) return -1;
   struct job j;
   memset(&j, 0, sizeof j);
+  j.arena = data;
+  j.nbytes = nbytes;
+  j.bs = bs;
+  j.out = out;
+  j.n = (size_t)((nbytes + bs - 1) / bs);
+  return run(&j, threads);
+}
+
+/* Hashes::hash_file(HashType::sha512_256(), bs, ..) over a memory buffer */
+int oracle_sha_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint8_t* out,
+                      int threads) {
+  if (bs == 0) return -1;
+  struct job j;
+  memset(&j, 0, sizeof j);
+  j.sha = 1;
   j.arena = data;
   j.nbytes = nbytes;
   j.bs = bs;

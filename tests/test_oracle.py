@@ -113,3 +113,21 @@ def test_sha512_256_oracle(oracle, dirsig_example):
     idx = dirsig_example["index"].encode()
     body = idx[idx.index(b"\n") + 1:-65]
     assert oracle_sha(oracle, body).hex().encode() == idx[-65:-1]
+
+
+def test_sha_chunks_threads_agree(oracle):
+    """oracle_sha_chunks (threaded SHA-512/256 block split, bench.py's
+    config2sha checker / CPU baseline) against hashlib."""
+    oracle.oracle_sha_chunks.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                         ctypes.c_void_p, ctypes.c_int]
+    rnd = random.Random(3)
+    for n, bs in [(0, 4096), (1, 4096), (111, 128), (112, 128), (5 * 4096 + 17, 4096),
+                  (70000, 32768)]:
+        data = bytes(rnd.randrange(256) for _ in range(n))
+        nb = (n + bs - 1) // bs
+        out = ctypes.create_string_buffer(32 * max(nb, 1))
+        buf = ctypes.create_string_buffer(data, max(n, 1))
+        for threads in (1, 3):
+            oracle.oracle_sha_chunks(buf, n, bs, out, threads)
+            assert out.raw[:32 * nb] == b"".join(
+                hashlib.new("sha512_256", data[i:i + bs]).digest() for i in range(0, n, bs))
