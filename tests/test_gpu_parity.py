@@ -200,8 +200,9 @@ def test_desc_mixed_ragged_shuffled(gpu, ctx, oracle):
 
 def test_desc_large_batch_exclusive_quad(gpu, ctx, oracle):
     """A batch above the small-batch limit (>= 49153 descriptors) with long
-    chains: the quad part runs SIMD-exclusive (k_quad_long<_, true>, launched
-    before a delayed lane part), the rest in lane mode; chain lengths on both
+    chains: the quad part runs SIMD-exclusive (k_quad_long<_, true>, started
+    on the long-chain list before the sort, the lane part gated on its
+    workgroups), the rest in lane mode; chain lengths on both
     sides of the 1024-line threshold, odd and even line counts, ragged
     tails, 16-B aligned and misaligned starts."""
     import torch
@@ -228,6 +229,40 @@ def test_desc_large_batch_exclusive_quad(gpu, ctx, oracle):
     want = np.zeros(32 * len(lens), dtype=np.uint8)
     oracle.oracle_hash_blocks(host.ctypes.data, ao.ctypes.data, al.ctypes.data, len(lens),
                               want.ctypes.data, 8)
+    assert first_bad(out.cpu().numpy(), want) is None
+
+
+def test_desc_quad_list_overflow(gpu, ctx, oracle):
+    """More long chains than the quad part holds (n_long > 64 x 256 = 16384
+    chains of >= 128 KiB in a batch of >= 49153): the quad part started on
+    the long-chain list before the sort stands down, and the longest 16384
+    chains of the sorted order run in quad mode after the sort (kQuadLate),
+    the rest in lane mode -- every chain hashed exactly once."""
+    import torch
+    rng = random.Random(0x0F10)
+    q = 1024 * 128
+    lens = [rng.choice([q, q + 1, q + 4096, 2 * q - 3]) for _ in range(17000)]
+    lens += [rng.randrange(0, 4097) for _ in range(40000)]
+    rng.shuffle(lens)
+    offs, pos = [], 0
+    for ln in lens:
+        pos += (-pos) % 16
+        offs.append(pos)
+        pos += ln
+    data = dev_random(gpu, pos, seed=43)
+    d_off = torch.tensor(offs, dtype=torch.int64, device="cuda:0")
+    d_len = torch.tensor(lens, dtype=torch.int32, device="cuda:0")
+    out = torch.zeros(32 * len(lens), dtype=torch.uint8, device="cuda:0")
+    ctx.hash_blocks_dev(data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), len(lens),
+                        out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    host = data.cpu().numpy()
+    del data
+    ao = np.array(offs, dtype=np.uint64)
+    al = np.array(lens, dtype=np.uint32)
+    want = np.zeros(32 * len(lens), dtype=np.uint8)
+    oracle.oracle_hash_blocks(host.ctypes.data, ao.ctypes.data, al.ctypes.data, len(lens),
+                              want.ctypes.data, 16)
     assert first_bad(out.cpu().numpy(), want) is None
 
 
