@@ -32,6 +32,9 @@
 #include "uniform.hpp"
 #include "sha512_dev.hpp"
 
+#define CIR_STR2(x) #x
+#define CIR_STR(x) CIR_STR2(x)
+
 #ifndef CIR_QUAD_EXCLUSIVE
 #define CIR_QUAD_EXCLUSIVE 1
 #endif
@@ -324,6 +327,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ chains, uint32_t* count,
     uint32_t nq_wg, int src, uint8_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWaves * kQuadWaveLds];
+#ifdef CIR_QPAD  // code-layout probe: CIR_QPAD 4-byte s_nop's ahead of the body
+  asm volatile(".rept " CIR_STR(CIR_QPAD) "\ns_nop 0\n.endr");
+#endif
   if constexpr (kExclusive) {
     asm volatile("v_accvgpr_write_b32 a255, 0" ::: "a255");
     // this workgroup holds its CU: count it for k_gate (count[1])
