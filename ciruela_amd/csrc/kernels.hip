@@ -306,44 +306,33 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))
                    wave * kQuadWaveLds);
 }
 
-// Quad part of an ordered batch: nl = min(*n_long, 64 nq_wg) chains.
+// Quad part of an ordered batch: chains [0, nl), nl = min(*n_long, 64 nq_wg).
 // Latency-bound (one 1 MiB chain = 8192 dependent compressions), so it keeps
 // a line's 40 message words in registers and runs at s_setprio 3; it is its
 // own kernel so the lane part keeps its occupancy.  kExclusive: each wave
 // touches a255, so it holds the SIMD's whole 512-register file and no lane
 // wave can share its SIMD (batches with a lane part beside the quad part).
-// Where the chains come from (src):
-//   kQuadSorted: chains = sorted[0, nl) (small batches: after the sort);
-//   kQuadEarly:  chains = the long-chain list, launched before the sort --
-//                only when every long chain fits (n_long <= 64 nq_wg), in
-//                which case the quad part runs in one round and the order of
-//                its chains does not matter;
-//   kQuadLate:   chains = sorted[0, nl), launched after the sort -- only
-//                when the list overflowed (n_long > 64 nq_wg).
-enum QuadSrc : int { kQuadSorted = 0, kQuadEarly = 1, kQuadLate = 2 };
 template <bool kAsm, bool kExclusive>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_quad_long(
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ off,
-    const uint32_t* __restrict__ len, const uint32_t* __restrict__ chains, uint32_t* count,
-    uint32_t nq_wg, int src, uint8_t* __restrict__ out) {
+    const uint32_t* __restrict__ len, const uint32_t* __restrict__ perm, uint32_t* n_long,
+    uint32_t nq_wg, uint8_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWaves * kQuadWaveLds];
 #ifdef CIR_QPAD  // code-layout probe: CIR_QPAD 4-byte s_nop's ahead of the body
   asm volatile(".rept " CIR_STR(CIR_QPAD) "\ns_nop 0\n.endr");
 #endif
   if constexpr (kExclusive) {
     asm volatile("v_accvgpr_write_b32 a255, 0" ::: "a255");
-    // this workgroup holds its CU: count it for k_gate (count[1])
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(count + 1, 1u, __ATOMIC_RELAXED,
+    // this workgroup holds its CU: count it for k_gate (n_long[1])
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(n_long + 1, 1u, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
   }
-  const uint32_t n_long = *count, cap = nq_wg * 64u;
-  if ((src == kQuadEarly && n_long > cap) || (src == kQuadLate && n_long <= cap)) return;
-  const uint32_t nl = min(n_long, cap);
+  const uint32_t nl = min(*n_long, nq_wg * 64u);
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t first = (blockIdx.x * kWaves + wave) * 16u;
   if (first >= nl) return;
   __builtin_amdgcn_s_setprio(3);
-  quad_chains<true, kAsm>(arena, off, len, chains, first, nl, out, lds, wave * kQuadWaveLds);
+  quad_chains<true, kAsm>(arena, off, len, perm, first, nl, out, lds, wave * kQuadWaveLds);
 }
 
 // The lane part of an exclusive mixed batch waits until every quad
@@ -645,7 +634,7 @@ hipError_t launch_general_desc(const uint8_t* arena, const uint64_t* off, const 
 }
 
 hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
-                        uint64_t n, uint8_t* out, OrderView* ov, size_t scratch_bytes,
+                        const uint32_t* perm, uint32_t* n_long, uint64_t n, uint8_t* out,
                         hipStream_t s, hipStream_t qs, hipStream_t aux, hipEvent_t fork,
                         hipEvent_t qjoin, hipEvent_t ljoin) {
   if (n == 0) return hipSuccess;
@@ -653,55 +642,31 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
   const uint64_t lane_grid = grid_for(n, kThreads);
   if (lane_grid > 0x7fffffffull) return hipErrorInvalidValue;
   const bool exclusive = CIR_QUAD_EXCLUSIVE && n >= kQuadSmallBatch;
-  uint32_t* count = ov->count;
-  hipError_t e = hipSuccess;
-  auto fork_to = [&](hipStream_t t) {
-    // a wait captures the event's latest record, so `fork` can be re-recorded
-    if (e == hipSuccess && t != s) e = hipEventRecord(fork, s);
-    if (e == hipSuccess && t != s) e = hipStreamWaitEvent(t, fork, 0);
-  };
+  hipError_t e = hipEventRecord(fork, s);
+  if (e == hipSuccess && qs != s) e = hipStreamWaitEvent(qs, fork, 0);
+  if (e == hipSuccess && aux != s) e = hipStreamWaitEvent(aux, fork, 0);
+  if (e != hipSuccess) return e;
   if (exclusive) {
     // The quad workgroups need whole CUs (one 504-register wave per SIMD):
-    // they start on the long-chain list right after the keys, before the
-    // sort; the lane part starts once all of them hold their CUs (k_gate),
-    // so its waves fill the other CUs instead of taking every SIMD first.
-    fork_to(qs);
-    if (e != hipSuccess) return e;
+    // they are dispatched first, and the lane part starts once all of them
+    // hold their CUs (k_gate), so its waves fill the other CUs instead of
+    // taking every SIMD first.
     hipLaunchKernelGGL((k_quad_long<kQuadAsm, true>), dim3((unsigned)nq), dim3(kThreads), 0, qs,
-                       arena, off, len, (const uint32_t*)ov->long_list, count, (uint32_t)nq,
-                       (int)kQuadEarly, out);
+                       arena, off, len, perm, n_long, (uint32_t)nq, out);
     e = hipGetLastError();
-    if (e == hipSuccess) e = launch_order_sort(ov, scratch_bytes, s);
-    // the rare overflow (more long chains than 64 nq): the longest 64 nq
-    // chains of the sorted order, after the sort
-    fork_to(qs);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_quad_long<kQuadAsm, true>), dim3((unsigned)nq), dim3(kThreads), 0, qs,
-                       arena, off, len, (const uint32_t*)ov->perm, count, (uint32_t)nq,
-                       (int)kQuadLate, out);
-    e = hipGetLastError();
-    fork_to(aux);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, aux, (const uint32_t*)(count + 1),
-                       (uint32_t)nq, 600u);
+    hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, aux, n_long + 1, (uint32_t)nq, 600u);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads), 0, aux, arena, off,
-                       len, (const uint32_t*)ov->perm, n, (const uint32_t*)count, (uint32_t)nq,
-                       out);
+                       len, perm, n, n_long, (uint32_t)nq, out);
   } else {
-    e = launch_order_sort(ov, scratch_bytes, s);
-    fork_to(aux);
-    fork_to(qs);
-    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads), 0, aux, arena, off,
-                       len, (const uint32_t*)ov->perm, n, (const uint32_t*)count, (uint32_t)nq,
-                       out);
+                       len, perm, n, n_long, (uint32_t)nq, out);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_quad_long<kQuadAsm, false>), dim3((unsigned)nq), dim3(kThreads), 0, qs,
-                       arena, off, len, (const uint32_t*)ov->perm, count, (uint32_t)nq,
-                       (int)kQuadSorted, out);
+                       arena, off, len, perm, n_long, (uint32_t)nq, out);
   }
   e = hipGetLastError();
   if (e == hipSuccess && qs != s) e = hipEventRecord(qjoin, qs);

@@ -67,38 +67,22 @@ hipError_t launch_general_chunks(const uint8_t* data, uint64_t nbytes, uint64_t 
 hipError_t launch_general_desc(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
                                const uint32_t* perm, uint64_t n, uint8_t* out, hipStream_t s);
 
-// Device buffers of one ordered descriptor batch (order.hip), all inside the
-// caller's ordering scratch.
-struct OrderView {
-  uint32_t* count = nullptr;      // [0] = n_long, [1] = quad workgroups started
-  uint16_t* key_in = nullptr;
-  uint16_t* key_out = nullptr;
-  uint32_t* idx_in = nullptr;
-  uint32_t* idx_out = nullptr;
-  uint32_t* long_list = nullptr;  // the n_long long chains, arbitrary order
-  uint32_t* perm = nullptr;       // longest chain first (valid after the sort)
-  void* temp = nullptr;
-  uint64_t n = 0;
-};
-
-size_t order_scratch_bytes(uint64_t n);
-// Counters reset, keys, the long-chain list (chains of >= quad_min_lines(n)
-// lines) and their count, on s.
-hipError_t launch_order_keys(const uint32_t* len, uint64_t n, void* scratch, size_t bytes,
-                             OrderView* ov, hipStream_t s);
-// The longest-chain-first sort into ov->perm, on s.
-hipError_t launch_order_sort(OrderView* ov, size_t bytes, hipStream_t s);
-
-// A BLAKE2b descriptor batch after launch_order_keys: the first
-// min(n_long, 64 * quad_max_wg(n)) chains run in quad mode on qs, the rest
-// one lane per chain on `aux` through the sorted order; everything forks
-// from s and joins back into it (events `fork`, `qjoin`, `ljoin`).  In
-// large batches the quad part starts before the sort (on the long-chain
-// list) and the lane part waits until the quad workgroups hold their CUs.
+// Descriptor batch in the order perm (longest chain first); the first
+// min(*n_long, 64 * quad_max_wg(n)) chains (device count) run in quad mode on
+// qs, the rest one lane per chain on `aux`; both fork from s (`fork`) and
+// join back into s (`qjoin`, `ljoin`).
 hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
-                        uint64_t n, uint8_t* out, OrderView* ov, size_t scratch_bytes,
+                        const uint32_t* perm, uint32_t* n_long, uint64_t n, uint8_t* out,
                         hipStream_t s, hipStream_t qs, hipStream_t aux, hipEvent_t fork,
                         hipEvent_t qjoin, hipEvent_t ljoin);
+
+// Longest-chain-first order of a descriptor batch (order.hip): *perm points
+// into `scratch` (order_scratch_bytes(n) bytes, device memory).
+size_t order_scratch_bytes(uint64_t n);
+// *n_long = number of chains with >= quad_min_lines(n) lines (device memory);
+// (*n_long)[1] = 0, the started-workgroup counter of the quad part.
+hipError_t launch_order_desc(const uint32_t* len, uint64_t n, void* scratch, size_t bytes,
+                             uint32_t** perm, uint32_t** n_long, hipStream_t s);
 
 // SHA-512/256 per descriptor (one lane per block), digest b -> out + 32 b.
 hipError_t launch_sha_desc(const uint8_t* arena, const uint64_t* off, const uint32_t* len,

@@ -218,16 +218,14 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
     d.order_cap = need;
   }
   CIR_HIP(hipStreamWaitEvent(s, d.order_free, 0));
-  dev::OrderView ov;
-  CIR_HIP(dev::launch_order_keys(len, n, d.order_scratch, d.order_cap, &ov, s));
-  if (ht == CIR_HASH_SHA512_256) {
-    CIR_HIP(dev::launch_order_sort(&ov, d.order_cap, s));
-    CIR_HIP(dev::launch_sha_desc(arena, off, len, ov.perm, n, out, s));
-  } else {
-    CIR_HIP(dev::launch_mixed(arena, off, len, n, out, &ov, d.order_cap, s,
-                              d.qstream ? d.qstream : s, d.aux ? d.aux : s, d.aux_fork, d.q_join,
-                              d.aux_join));
-  }
+  uint32_t* perm = nullptr;
+  uint32_t* n_long = nullptr;
+  CIR_HIP(dev::launch_order_desc(len, n, d.order_scratch, d.order_cap, &perm, &n_long, s));
+  if (ht == CIR_HASH_SHA512_256)
+    CIR_HIP(dev::launch_sha_desc(arena, off, len, perm, n, out, s));
+  else
+    CIR_HIP(dev::launch_mixed(arena, off, len, perm, n_long, n, out, s, d.qstream ? d.qstream : s,
+                              d.aux ? d.aux : s, d.aux_fork, d.q_join, d.aux_join));
   CIR_HIP(hipEventRecord(d.order_free, s));
   return CIR_OK;
 }

@@ -200,9 +200,8 @@ def test_desc_mixed_ragged_shuffled(gpu, ctx, oracle):
 
 def test_desc_large_batch_exclusive_quad(gpu, ctx, oracle):
     """A batch above the small-batch limit (>= 49153 descriptors) with long
-    chains: the quad part runs SIMD-exclusive (k_quad_long<_, true>, started
-    on the long-chain list before the sort, the lane part gated on its
-    workgroups), the rest in lane mode; chain lengths on both
+    chains: the quad part runs SIMD-exclusive (k_quad_long<_, true>, launched
+    before a delayed lane part), the rest in lane mode; chain lengths on both
     sides of the 1024-line threshold, odd and even line counts, ragged
     tails, 16-B aligned and misaligned starts."""
     import torch
@@ -232,12 +231,11 @@ def test_desc_large_batch_exclusive_quad(gpu, ctx, oracle):
     assert first_bad(out.cpu().numpy(), want) is None
 
 
-def test_desc_quad_list_overflow(gpu, ctx, oracle):
+def test_desc_quad_capacity_overflow(gpu, ctx, oracle):
     """More long chains than the quad part holds (n_long > 64 x 256 = 16384
-    chains of >= 128 KiB in a batch of >= 49153): the quad part started on
-    the long-chain list before the sort stands down, and the longest 16384
-    chains of the sorted order run in quad mode after the sort (kQuadLate),
-    the rest in lane mode -- every chain hashed exactly once."""
+    chains of >= 128 KiB in a batch of >= 49153): the longest 16384 chains of
+    the sorted order run in quad mode, every other one (long ones included)
+    in lane mode -- every chain hashed exactly once."""
     import torch
     rng = random.Random(0x0F10)
     q = 1024 * 128
