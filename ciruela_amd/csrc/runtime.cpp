@@ -73,6 +73,17 @@ Device::~Device() {
   if (copy) (void)hipStreamDestroy(copy);
 }
 
+// CIR_ZERO_COPY=1: the staged host paths hand the pinned staging buffers to
+// the hash kernels directly (PCIe reads from the kernels) instead of an SDMA
+// copy into device memory first (A/B: profiles/r02/).
+bool zero_copy() {
+  static const bool on = [] {
+    const char* v = std::getenv("CIR_ZERO_COPY");
+    return v && *v && strcmp(v, "0") != 0;
+  }();
+  return on;
+}
+
 bool trace_enabled() {
   static const bool on = [] {
     const char* v = std::getenv("CIR_TRACE");
@@ -97,8 +108,12 @@ int Device::ensure_slot(Slot& s, uint64_t bytes, uint64_t nblk) {
     s.h_data = nullptr;
     s.d_data = nullptr;
     s.cap = 0;
-    CIR_HIP(hipHostMalloc(&s.h_data, bytes, hipHostMallocDefault));
-    CIR_HIP(hipMalloc(&s.d_data, bytes));
+    // zero-copy: the kernels read the staging buffer over PCIe, so it must be
+    // coherent (not cached by the GPU between the batches that reuse it)
+    CIR_HIP(hipHostMalloc(&s.h_data, bytes,
+                          zero_copy() ? hipHostMallocMapped | hipHostMallocCoherent
+                                      : hipHostMallocDefault));
+    if (!zero_copy()) CIR_HIP(hipMalloc(&s.d_data, bytes));
     s.cap = bytes;
   }
   if (nblk > s.cap_blk) {
@@ -236,7 +251,10 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
 static int slot_submit_impl(Device& d, Slot& s, uint64_t bytes, uint64_t nblk,
                             uint64_t chunk_bs, int ht) {
   if (s.t_copy0) CIR_HIP(hipEventRecord(s.t_copy0, d.copy));
-  CIR_HIP(hipMemcpyAsync(s.d_data, s.h_data, bytes, hipMemcpyHostToDevice, d.copy));
+  // zero-copy: the hash kernels read the pinned slot over PCIe themselves
+  const uint8_t* src = zero_copy() ? s.h_data : s.d_data;
+  if (!zero_copy())
+    CIR_HIP(hipMemcpyAsync(s.d_data, s.h_data, bytes, hipMemcpyHostToDevice, d.copy));
   if (chunk_bs == 0) {
     CIR_HIP(hipMemcpyAsync(s.d_off, s.h_off, nblk * 8, hipMemcpyHostToDevice, d.copy));
     CIR_HIP(hipMemcpyAsync(s.d_len, s.h_len, nblk * 4, hipMemcpyHostToDevice, d.copy));
@@ -246,10 +264,10 @@ static int slot_submit_impl(Device& d, Slot& s, uint64_t bytes, uint64_t nblk,
   CIR_HIP(hipStreamWaitEvent(d.compute, s.copied, 0));
   if (s.t_hash0) CIR_HIP(hipEventRecord(s.t_hash0, d.compute));
   if (chunk_bs == 0) {
-    int rc = hash_desc_ordered(d, s.d_data, s.d_off, s.d_len, nblk, s.d_out, d.compute, ht);
+    int rc = hash_desc_ordered(d, src, s.d_off, s.d_len, nblk, s.d_out, d.compute, ht);
     if (rc) return rc;
   } else
-    CIR_HIP(dev::launch_chunks(s.d_data, bytes, chunk_bs, s.d_out, d.compute));
+    CIR_HIP(dev::launch_chunks(src, bytes, chunk_bs, s.d_out, d.compute));
   CIR_HIP(hipMemcpyAsync(s.h_out, s.d_out, nblk * 32, hipMemcpyDeviceToHost, d.compute));
   CIR_HIP(hipEventRecord(s.done, d.compute));
   s.busy = true;

@@ -66,6 +66,8 @@ struct Slot {
 
 // CIR_TRACE set to a non-empty value other than "0": per-batch timings on stderr.
 bool trace_enabled();
+// CIR_ZERO_COPY: hash kernels read the pinned staging slots directly.
+bool zero_copy();
 
 struct Device {
   int id = 0;
