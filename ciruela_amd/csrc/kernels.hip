@@ -44,6 +44,10 @@ namespace dev {
 
 static inline unsigned grid_for(uint64_t n, uint64_t per) { return (unsigned)((n + per - 1) / per); }
 
+#ifdef CIR_QUAD_CLOCK
+__device__ unsigned long long g_quad_clock[3];
+#endif
+
 // Pure uniform launch: nblk = gridDim.x * 256 equal blocks.
 __global__ __launch_bounds__(kThreads, 5) void k_uniform_glds(const uint8_t* __restrict__ data,
                                                                uint64_t bs, uint32_t lines,
@@ -332,7 +336,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))
   const uint32_t first = (blockIdx.x * kWaves + wave) * 16u;
   if (first >= nl) return;
   __builtin_amdgcn_s_setprio(3);
+#ifdef CIR_QUAD_CLOCK  // diagnostics build: per-wave shader clock / 100 MHz clock
+  const uint64_t c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+#endif
   quad_chains<true, kAsm>(arena, off, len, perm, first, nl, out, lds, wave * kQuadWaveLds);
+#ifdef CIR_QUAD_CLOCK
+  const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63u) == 0) {
+    atomicAdd(&g_quad_clock[0], (unsigned long long)(c1 - c0));
+    atomicAdd(&g_quad_clock[1], (unsigned long long)(r1 - r0));
+    atomicAdd(&g_quad_clock[2], 1ull);
+  }
+#endif
 }
 
 // The lane part of an exclusive mixed batch waits until every quad
@@ -352,20 +367,54 @@ __global__ void k_gate(const uint32_t* started, uint32_t target, uint32_t max_ro
 }
 
 // Lane part: chains [nl, n) of the order, one lane per chain.
+//
+// Pacing (pace != 0, exclusive mixed batches): the quad part's longest chain
+// sets the batch's time, and whatever else runs meanwhile lowers the chip's
+// clock -- beside a full-width lane part the quad waves ran at 2.20 GHz
+// instead of 2.39 alone (profiles/r02/lane_pacing/).  So when every long
+// chain is in the quad part, only as many lane workgroups run as finish the
+// lane work (count[4..5]) within the longest quad chain (count[2]) at `pace`
+// lane compressions per workgroup per quad compression; the other
+// workgroups exit at once.  Waves claim tiles of 64 chains of the order from
+// count[6], so a helper launch of this kernel behind the quad part (pace 0)
+// finishes whatever the paced part left when the quad part ended: a pace
+// set too high costs the leftover's time on the whole chip instead of
+// stretching the lane part past the quad part.  Config 3, one library, one
+// process per value (profiles/r02/lane_pacing/pace_sweep.log): pace 0 826
+// GiB/s, 40 863, 48 871, 52 877-887, 60 896, 80 878-880 (without the
+// helper, 56 fell to 771).
+#ifndef CIR_LANE_PACE
+#define CIR_LANE_PACE 60
+#endif
 __global__ __launch_bounds__(kThreads, 4) void k_lane_rest(const uint8_t* __restrict__ arena,
                                                             const uint64_t* __restrict__ off,
                                                             const uint32_t* __restrict__ len,
                                                             const uint32_t* __restrict__ perm,
-                                                            uint64_t n, const uint32_t* n_long,
-                                                            uint32_t nq_wg,
+                                                            uint64_t n, uint32_t* count,
+                                                            uint32_t nq_wg, uint32_t pace,
                                                             uint8_t* __restrict__ out) {
-  const uint32_t nl = min(*n_long, nq_wg * 64u);
-  const uint64_t j = nl + (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (j >= n) return;
-  const uint32_t b = perm[j];
-  uint64_t h[8];
-  hash_chain(arena + off[b], len[b], h);
-  store_digest(out + (uint64_t)b * 32u, h);
+  const uint32_t nlong = count[0];
+  const uint32_t nl = min(nlong, nq_wg * 64u);
+  if (pace != 0 && nlong > 0 && nlong <= nq_wg * 64u) {
+    const uint64_t lq = (uint64_t)count[2] * pace;
+    const uint64_t work = *reinterpret_cast<const unsigned long long*>(count + 4);
+    if (blockIdx.x >= max<uint64_t>(1, (work + lq - 1) / lq)) return;
+  }
+  const uint32_t lane = threadIdx.x & 63u;
+  for (;;) {
+    uint32_t t = 0;
+    if (lane == 0) t = atomicAdd(count + 6, 1u);
+    t = __builtin_amdgcn_readfirstlane(t);
+    const uint64_t j0 = nl + (uint64_t)t * 64u;
+    if (j0 >= n) break;
+    const uint64_t j = j0 + lane;
+    if (j < n) {
+      const uint32_t b = perm[j];
+      uint64_t h[8];
+      hash_chain(arena + off[b], len[b], h);
+      store_digest(out + (uint64_t)b * 32u, h);
+    }
+  }
 }
 
 // Resumable single chain (the index footer, fed incrementally): one quad.
@@ -641,6 +690,11 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
   const uint64_t nq = std::min<uint64_t>((n + 63) / 64, quad_max_wg(n));
   const uint64_t lane_grid = grid_for(n, kThreads);
   if (lane_grid > 0x7fffffffull) return hipErrorInvalidValue;
+  static const uint32_t pace_env = [] {  // CIR_LANE_PACE=N overrides (0: no pacing)
+    const char* v = getenv("CIR_LANE_PACE");
+    return v ? (uint32_t)strtoul(v, nullptr, 10) : (uint32_t)CIR_LANE_PACE;
+  }();
+  const uint32_t pace = aux != qs ? pace_env : 0u;  // only beside a concurrent quad part
   const bool exclusive = CIR_QUAD_EXCLUSIVE && n >= kQuadSmallBatch;
   hipError_t e = hipEventRecord(fork, s);
   if (e == hipSuccess && qs != s) e = hipStreamWaitEvent(qs, fork, 0);
@@ -659,10 +713,16 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads), 0, aux, arena, off,
-                       len, perm, n, n_long, (uint32_t)nq, out);
+                       len, perm, n, n_long, (uint32_t)nq, pace, out);
+    if (pace != 0) {  // helper behind the quad part: the paced part's leftover
+      e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads), 0, qs, arena,
+                         off, len, perm, n, n_long, (uint32_t)nq, 0u, out);
+    }
   } else {
     hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads), 0, aux, arena, off,
-                       len, perm, n, n_long, (uint32_t)nq, out);
+                       len, perm, n, n_long, (uint32_t)nq, 0u, out);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_quad_long<kQuadAsm, false>), dim3((unsigned)nq), dim3(kThreads), 0, qs,
@@ -688,3 +748,13 @@ hipError_t launch_fill_splitmix64(uint64_t* p, uint64_t nwords, uint64_t seed,
 
 }  // namespace dev
 }  // namespace cir
+
+#ifdef CIR_QUAD_CLOCK
+// Diagnostics build only: sums of the quad waves' (shader cycles, 100 MHz
+// ticks, waves) since the last call; resets them.
+extern "C" int cir_debug_quad_clock(unsigned long long* out3) {
+  if (hipMemcpyFromSymbol(out3, HIP_SYMBOL(cir::dev::g_quad_clock), 24) != hipSuccess) return -1;
+  static const unsigned long long zero[3] = {0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(cir::dev::g_quad_clock), zero, 24) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -80,7 +80,10 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
 // into `scratch` (order_scratch_bytes(n) bytes, device memory).
 size_t order_scratch_bytes(uint64_t n);
 // *n_long = number of chains with >= quad_min_lines(n) lines (device memory);
-// (*n_long)[1] = 0, the started-workgroup counter of the quad part.
+// (*n_long)[1] = 0, the started-workgroup counter of the quad part;
+// (*n_long)[2] = the longest chain's compressions; (*n_long)[4..5] (u64) =
+// the other chains' compressions + kLaneChainCost each.
+constexpr uint32_t kLaneChainCost = 4;
 hipError_t launch_order_desc(const uint32_t* len, uint64_t n, void* scratch, size_t bytes,
                              uint32_t** perm, uint32_t** n_long, hipStream_t s);
 

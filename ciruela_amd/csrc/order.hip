@@ -16,7 +16,7 @@ constexpr int kKeyBits = 16;  // k_chain_keys' key width
 
 __global__ void k_chain_keys(const uint32_t* __restrict__ len, uint64_t n, uint32_t min_lines,
                              uint16_t* __restrict__ key, uint32_t* __restrict__ idx,
-                             uint32_t* __restrict__ n_long) {
+                             uint32_t* __restrict__ count) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t l = len[i];
@@ -30,7 +30,16 @@ __global__ void k_chain_keys(const uint32_t* __restrict__ len, uint64_t n, uint3
   // (profiles/r02/gtrace*).
   key[i] = (uint16_t)(k < 32768u ? k : 32768u + ((k - 32768u) >> 10));
   idx[i] = (uint32_t)i;
-  if (k >= min_lines) atomicAdd(n_long, 1u);
+  // count[0] = long chains, count[2] = the longest chain (compressions),
+  // count[4..5] = the lane part's work (launch_mixed's pacing): compressions
+  // plus kLaneChainCost per chain for its setup and digest store
+  if (k >= min_lines) {
+    atomicAdd(count, 1u);
+  } else {
+    atomicAdd(reinterpret_cast<unsigned long long*>(count + 4),
+              (unsigned long long)(k + kLaneChainCost));
+  }
+  atomicMax(count + 2, k);
 }
 
 size_t order_scratch_bytes(uint64_t n) {
@@ -47,8 +56,9 @@ hipError_t launch_order_desc(const uint32_t* len, uint64_t n, void* scratch, siz
   uint32_t* count = static_cast<uint32_t*>(scratch);
   uint8_t* p = static_cast<uint8_t*>(scratch) + 256;
   bytes -= 256;
-  // count[0] = n_long; count[1] = quad workgroups started (launch_mixed's gate)
-  hipError_t e0 = hipMemsetAsync(count, 0, 8, s);
+  // count[0] = n_long; count[1] = quad workgroups started (launch_mixed's
+  // gate); count[2] = longest chain; count[4..5] = lane work (k_chain_keys)
+  hipError_t e0 = hipMemsetAsync(count, 0, 32, s);
   if (e0 != hipSuccess) return e0;
   *n_long = count;
   uint16_t* key_in = reinterpret_cast<uint16_t*>(p);

@@ -231,6 +231,35 @@ def test_desc_large_batch_exclusive_quad(gpu, ctx, oracle):
     assert first_bad(out.cpu().numpy(), want) is None
 
 
+def test_desc_paced_lane_part_single_workgroup(gpu, ctx, oracle):
+    """Lane pacing at its extreme: 64 chains of 1 MiB (quad part) beside
+    60000 chains of 0..200 bytes, so the paced lane part runs ~1 workgroup
+    that strides over every short chain (k_lane_rest, count[2], count[4..5])."""
+    import torch
+    rng = random.Random(0x9ACE)
+    lens = [1 << 20] * 64 + [rng.randrange(0, 201) for _ in range(60000)]
+    rng.shuffle(lens)
+    offs, pos = [], 0
+    for i, ln in enumerate(lens):
+        pos += (-pos) % 16 + (5 if i % 13 == 0 else 0)
+        offs.append(pos)
+        pos += ln
+    data = dev_random(gpu, pos, seed=47)
+    d_off = torch.tensor(offs, dtype=torch.int64, device="cuda:0")
+    d_len = torch.tensor(lens, dtype=torch.int32, device="cuda:0")
+    out = torch.zeros(32 * len(lens), dtype=torch.uint8, device="cuda:0")
+    ctx.hash_blocks_dev(data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), len(lens),
+                        out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    host = data.cpu().numpy()
+    ao = np.array(offs, dtype=np.uint64)
+    al = np.array(lens, dtype=np.uint32)
+    want = np.zeros(32 * len(lens), dtype=np.uint8)
+    oracle.oracle_hash_blocks(host.ctypes.data, ao.ctypes.data, al.ctypes.data, len(lens),
+                              want.ctypes.data, 8)
+    assert first_bad(out.cpu().numpy(), want) is None
+
+
 def test_desc_quad_capacity_overflow(gpu, ctx, oracle):
     """More long chains than the quad part holds (n_long > 64 x 256 = 16384
     chains of >= 128 KiB in a batch of >= 49153): the longest 16384 chains of
