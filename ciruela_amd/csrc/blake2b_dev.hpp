@@ -586,6 +586,59 @@ __device__ __forceinline__ void compress_quad_asm(uint64_t& a, uint64_t& b, uint
                : "vcc");
 }
 
+// The same compression with the NEXT line's 40 message words read from LDS
+// inside the block: two ds_read_b64 after each of the first 20 G steps, into
+// `next` (addresses pa: LDS byte addresses), and lgkmcnt(0) at the end (the
+// last reads issued 4 G steps, ~400 cycles, earlier), so nothing is in
+// flight when the block ends.  A wave alone issues in order: 40 reads in a
+// row before the block held its VALU idle for their issue; between VALU
+// instructions they issue while the VALU works.
+#define CIR_RD2(K0, K1) "ds_read_b64 %[n" #K0 "], %[p" #K0 "]\nds_read_b64 %[n" #K1 "], %[p" #K1 "]\n"
+#define CIR_QR_RD(K0, K1, K2, K3)                                             \
+  CIR_QG_DPP(CIR_QP_93, CIR_QP_4E, CIR_QP_39, CIR_M(K0), CIR_M(K1))           \
+  CIR_RD2(K0, K1)                                                             \
+  CIR_QG_DPP(CIR_QP_39, CIR_QP_4E, CIR_QP_93, CIR_M(K2), CIR_M(K3))           \
+  CIR_RD2(K2, K3)
+#define CIR_QCOMPRESS_RD                                                      \
+  CIR_QG_PLAIN(CIR_M(0), CIR_M(1)) CIR_RD2(0, 1)                              \
+  CIR_QG_DPP(CIR_QP_39, CIR_QP_4E, CIR_QP_93, CIR_M(2), CIR_M(3)) CIR_RD2(2, 3) \
+  CIR_QR_RD(4, 5, 6, 7) CIR_QR_RD(8, 9, 10, 11) CIR_QR_RD(12, 13, 14, 15)     \
+  CIR_QR_RD(16, 17, 18, 19) CIR_QR_RD(20, 21, 22, 23) CIR_QR_RD(24, 25, 26, 27) \
+  CIR_QR_RD(28, 29, 30, 31) CIR_QR_RD(32, 33, 34, 35) CIR_QR_RD(36, 37, 38, 39) \
+  CIR_QR(0, 1, 2, 3) CIR_QR(4, 5, 6, 7) "s_waitcnt lgkmcnt(0)\ns_nop 1\n"
+#define CIR_NO(k) [n##k] "=&v"(next[k])
+#define CIR_PA(k) [p##k] "v"(pa[k])
+
+__device__ __forceinline__ void compress_quad_asm_rd(uint64_t& a, uint64_t& b, uint64_t& c,
+                                                     uint64_t& d, const uint64_t (&m)[40],
+                                                     uint64_t (&next)[40],
+                                                     const uint32_t (&pa)[40]) {
+  uint64_t t, u;
+  asm volatile(CIR_QCOMPRESS_RD
+               : "+{v[40:41]}"(a), "+{v[42:43]}"(b), "+{v[44:45]}"(c), "+{v[46:47]}"(d),
+                 "=&{v[48:49]}"(t), "=&{v[50:51]}"(u), CIR_NO(0), CIR_NO(1), CIR_NO(2),
+                 CIR_NO(3), CIR_NO(4), CIR_NO(5), CIR_NO(6), CIR_NO(7), CIR_NO(8), CIR_NO(9),
+                 CIR_NO(10), CIR_NO(11), CIR_NO(12), CIR_NO(13), CIR_NO(14), CIR_NO(15),
+                 CIR_NO(16), CIR_NO(17), CIR_NO(18), CIR_NO(19), CIR_NO(20), CIR_NO(21),
+                 CIR_NO(22), CIR_NO(23), CIR_NO(24), CIR_NO(25), CIR_NO(26), CIR_NO(27),
+                 CIR_NO(28), CIR_NO(29), CIR_NO(30), CIR_NO(31), CIR_NO(32), CIR_NO(33),
+                 CIR_NO(34), CIR_NO(35), CIR_NO(36), CIR_NO(37), CIR_NO(38), CIR_NO(39)
+               : CIR_MO(0), CIR_MO(1), CIR_MO(2), CIR_MO(3), CIR_MO(4), CIR_MO(5), CIR_MO(6),
+                 CIR_MO(7), CIR_MO(8), CIR_MO(9), CIR_MO(10), CIR_MO(11), CIR_MO(12),
+                 CIR_MO(13), CIR_MO(14), CIR_MO(15), CIR_MO(16), CIR_MO(17), CIR_MO(18),
+                 CIR_MO(19), CIR_MO(20), CIR_MO(21), CIR_MO(22), CIR_MO(23), CIR_MO(24),
+                 CIR_MO(25), CIR_MO(26), CIR_MO(27), CIR_MO(28), CIR_MO(29), CIR_MO(30),
+                 CIR_MO(31), CIR_MO(32), CIR_MO(33), CIR_MO(34), CIR_MO(35), CIR_MO(36),
+                 CIR_MO(37), CIR_MO(38), CIR_MO(39), CIR_PA(0), CIR_PA(1), CIR_PA(2),
+                 CIR_PA(3), CIR_PA(4), CIR_PA(5), CIR_PA(6), CIR_PA(7), CIR_PA(8), CIR_PA(9),
+                 CIR_PA(10), CIR_PA(11), CIR_PA(12), CIR_PA(13), CIR_PA(14), CIR_PA(15),
+                 CIR_PA(16), CIR_PA(17), CIR_PA(18), CIR_PA(19), CIR_PA(20), CIR_PA(21),
+                 CIR_PA(22), CIR_PA(23), CIR_PA(24), CIR_PA(25), CIR_PA(26), CIR_PA(27),
+                 CIR_PA(28), CIR_PA(29), CIR_PA(30), CIR_PA(31), CIR_PA(32), CIR_PA(33),
+                 CIR_PA(34), CIR_PA(35), CIR_PA(36), CIR_PA(37), CIR_PA(38), CIR_PA(39)
+               : "vcc", "memory");
+}
+
 // One round of quad mode: column step (words x0, y0), diagonal step (x1, y1).
 // kFirst: round 0 (state in the column layout); kLast: round 11.
 template <bool kFirst, bool kLast>
@@ -681,6 +734,19 @@ __device__ __forceinline__ void compress_quad_regs(uint64_t& h0, uint64_t& h1,
                                                    uint64_t dv) {
   uint64_t a = h0, b = h1, c = cv, d = dv;
   compress_quad_asm(a, b, c, d, m);
+  const uint64_t cc = mk64(qd<kQuadFromNext2>(lo32(c)) ^ lo32(a), qd<kQuadFromNext2>(hi32(c)) ^ hi32(a));
+  h0 = h0 ^ cc;
+  const uint64_t bb = mk64(qd<kQuadFromPrev>(lo32(b)) ^ lo32(h1), qd<kQuadFromPrev>(hi32(b)) ^ hi32(h1));
+  h1 = mk64(qd<kQuadFromNext>(lo32(d)) ^ lo32(bb), qd<kQuadFromNext>(hi32(d)) ^ hi32(bb));
+}
+
+__device__ __forceinline__ void compress_quad_regs_rd(uint64_t& h0, uint64_t& h1,
+                                                      const uint64_t (&m)[40],
+                                                      uint64_t (&next)[40],
+                                                      const uint32_t (&pa)[40], uint64_t cv,
+                                                      uint64_t dv) {
+  uint64_t a = h0, b = h1, c = cv, d = dv;
+  compress_quad_asm_rd(a, b, c, d, m, next, pa);
   const uint64_t cc = mk64(qd<kQuadFromNext2>(lo32(c)) ^ lo32(a), qd<kQuadFromNext2>(hi32(c)) ^ hi32(a));
   h0 = h0 ^ cc;
   const uint64_t bb = mk64(qd<kQuadFromPrev>(lo32(b)) ^ lo32(h1), qd<kQuadFromPrev>(hi32(b)) ^ hi32(h1));

@@ -35,6 +35,16 @@
 #define CIR_STR2(x) #x
 #define CIR_STR(x) CIR_STR2(x)
 
+// Quad mode with the next line's LDS reads inside the compression's asm
+// block (kRdi, compress_quad_asm_rd): per kernel, as measured
+// (profiles/r02/quad_rdi/).
+#ifndef CIR_QUAD_RDI_CHUNKS
+#define CIR_QUAD_RDI_CHUNKS 1
+#endif
+#ifndef CIR_QUAD_RDI_LONG
+#define CIR_QUAD_RDI_LONG 0
+#endif
+
 #ifndef CIR_QUAD_EXCLUSIVE
 #define CIR_QUAD_EXCLUSIVE 1
 #endif
@@ -191,7 +201,7 @@ __device__ __forceinline__ void quad_init(uint32_t i, uint64_t& h0, uint64_t& h1
 // Advance a quad's chain over L bytes at p, t0 bytes already compressed.
 // final: the last line (partial, or the empty block of an empty input)
 // carries the final flag; otherwise L must be a multiple of 128.
-template <bool kPrefetchAll = false, bool kAsm = kQuadAsm>
+template <bool kPrefetchAll = false, bool kAsm = kQuadAsm, bool kRdi = false>
 __device__ __forceinline__ void quad_run(uint64_t& h0, uint64_t& h1, uint64_t t0,
                                          const uint8_t* p, uint32_t L, bool active, bool final,
                                          uint8_t* lds, const uint32_t (&addr)[48], uint32_t line,
@@ -229,6 +239,43 @@ __device__ __forceinline__ void quad_run(uint64_t& h0, uint64_t& h1, uint64_t t0
       const uint64_t dv = dv0 ^ (i == 0 ? t : 0ull) ^ ((i == 2 && last) ? ~0ull : 0ull);
       compress_quad_regs(h0, h1, m, cv, dv);
     };
+    if constexpr (kRdi) {
+      // The next line's 40 reads issue inside the compression's asm block
+      // (compress_quad_asm_rd), between its VALU instructions.
+      uint32_t pa[40];
+#pragma unroll
+      for (int k = 0; k < 40; ++k) pa[k] = (uint32_t)reinterpret_cast<uintptr_t>(lds) + addr[k];
+      auto put = [&](uint32_t it) {
+        *reinterpret_cast<uint4*>(lds + line + 32u * i) = u;
+        *reinterpret_cast<uint4*>(lds + line + 32u * i + 16u) = w;
+        if (it + 1 < total) fetch(it + 1, u, w);
+      };
+      auto step_rd = [&](uint32_t it, const uint64_t (&m)[40], uint64_t (&nx)[40]) {
+        const bool last = final && it + 1 == total;
+        const uint64_t t = t0 + (last ? (uint64_t)L : (uint64_t)(it + 1) * 128u);
+        const uint64_t dv = dv0 ^ (i == 0 ? t : 0ull) ^ ((i == 2 && last) ? ~0ull : 0ull);
+        compress_quad_regs_rd(h0, h1, m, nx, pa, cv, dv);
+      };
+      if (total) {
+        put(0);
+        quad_read_msg(ma, lds, addr);
+      }
+      for (uint32_t it = 0; it < total; it += 2) {
+        if (it + 1 >= total) {
+          step(it, ma);
+          break;
+        }
+        put(it + 1);
+        step_rd(it, ma, mb);
+        if (it + 2 >= total) {
+          step(it + 1, mb);
+          break;
+        }
+        put(it + 2);
+        step_rd(it + 1, mb, ma);
+      }
+      return;
+    }
     constexpr int kLgkm0 = 0xC07F;  // s_waitcnt lgkmcnt(0), vmcnt/expcnt untouched
     if (total) stage(0, ma);
     for (uint32_t it = 0; it < total; it += 2) {
@@ -257,7 +304,7 @@ __device__ __forceinline__ void quad_run(uint64_t& h0, uint64_t& h1, uint64_t t0
 
 // The chain of quad q of this wave (block b at p, L bytes; have = false for a
 // quad past the end) is hashed into out + 32 b.
-template <bool kPrefetchAll, bool kAsm = kQuadAsm>
+template <bool kPrefetchAll, bool kAsm = kQuadAsm, bool kRdi = false>
 __device__ __forceinline__ void quad_chain(bool have, uint64_t b, const uint8_t* p, uint32_t L,
                                            uint8_t* __restrict__ out, uint8_t* lds,
                                            uint32_t wave_lds) {
@@ -267,7 +314,7 @@ __device__ __forceinline__ void quad_chain(bool have, uint64_t b, const uint8_t*
   quad_addr(addr, line, i);
   uint64_t h0, h1;
   quad_init(i, h0, h1);
-  quad_run<kPrefetchAll, kAsm>(h0, h1, 0, p, have ? L : 0u, have, true, lds, addr, line, i);
+  quad_run<kPrefetchAll, kAsm, kRdi>(h0, h1, 0, p, have ? L : 0u, have, true, lds, addr, line, i);
   if (have) *reinterpret_cast<uint64_t*>(out + b * 32u + 8u * i) = h0;
 }
 
@@ -287,7 +334,7 @@ __device__ __forceinline__ void quad_chains(const uint8_t* __restrict__ arena,
     o = off[b];
     L = len[b];
   }
-  quad_chain<kPrefetchAll, kAsm>(have, b, arena + o, L, out, lds, wave_lds);
+  quad_chain<kPrefetchAll, kAsm, CIR_QUAD_RDI_LONG != 0>(have, b, arena + o, L, out, lds, wave_lds);
 }
 
 // Hashes::hash_file split of one device-resident file, blocks [b0, nblk):
@@ -306,7 +353,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))
   const bool have = b < nblk;
   const uint64_t o = have ? b * bs : 0;
   const uint64_t rest = nbytes - o;
-  quad_chain<true>(have, b, data + o, have ? (uint32_t)(rest < bs ? rest : bs) : 0u, out, lds,
+  quad_chain<true, kQuadAsm, CIR_QUAD_RDI_CHUNKS != 0>(have, b, data + o, have ? (uint32_t)(rest < bs ? rest : bs) : 0u, out, lds,
                    wave * kQuadWaveLds);
 }
 
