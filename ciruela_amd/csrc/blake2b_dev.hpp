@@ -504,6 +504,15 @@ __device__ __forceinline__ void g_quad(uint64_t& a, uint64_t& b, uint64_t& c, ui
 #define CIR_QUAD_ASM 1
 #endif
 constexpr bool kQuadAsm = CIR_QUAD_ASM != 0;
+// Every quad-mode asm block starts its 8-byte instructions on an 8-byte
+// boundary (the assembler pads with one s_nop 0 when needed; inside the
+// blocks the 4-byte instructions come in pairs).  A VOP2 DPP instruction
+// that straddles it issues ~10 % slower for a wave alone
+// (tools/align_ubench.hip), and the quad kernels moved 7-10 % with nothing
+// but their code offset (profiles/r02/quad_fast/ab_fastpad.log).
+#ifndef CIR_QALIGN
+#define CIR_QALIGN ".p2align 3\n"
+#endif
 #define CIR_QP_39 " quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf"
 #define CIR_QP_4E " quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"
 #define CIR_QP_93 " quad_perm:[3,0,1,2] row_mask:0xf bank_mask:0xf"
@@ -573,7 +582,7 @@ constexpr bool kQuadAsm = CIR_QUAD_ASM != 0;
 __device__ __forceinline__ void compress_quad_asm(uint64_t& a, uint64_t& b, uint64_t& c,
                                                   uint64_t& d, const uint64_t (&m)[40]) {
   uint64_t t, u;
-  asm volatile(CIR_QCOMPRESS
+  asm volatile(CIR_QALIGN CIR_QCOMPRESS
                : "+{v[40:41]}"(a), "+{v[42:43]}"(b), "+{v[44:45]}"(c), "+{v[46:47]}"(d),
                  "=&{v[48:49]}"(t), "=&{v[50:51]}"(u)
                : CIR_MO(0), CIR_MO(1), CIR_MO(2), CIR_MO(3), CIR_MO(4), CIR_MO(5), CIR_MO(6),
@@ -586,43 +595,74 @@ __device__ __forceinline__ void compress_quad_asm(uint64_t& a, uint64_t& b, uint
                : "vcc");
 }
 
-// The same compression with the NEXT line's 40 message words read from LDS
-// inside the block: two ds_read_b64 after each of the first 20 G steps, into
-// `next` (addresses pa: LDS byte addresses), and lgkmcnt(0) at the end (the
-// last reads issued 4 G steps, ~400 cycles, earlier), so nothing is in
-// flight when the block ends.  A wave alone issues in order: 40 reads in a
-// row before the block held its VALU idle for their issue; between VALU
-// instructions they issue while the VALU works.
-#define CIR_RD2(K0, K1) "ds_read_b64 %[n" #K0 "], %[p" #K0 "]\nds_read_b64 %[n" #K1 "], %[p" #K1 "]\n"
-#define CIR_QR_RD(K0, K1, K2, K3)                                             \
-  CIR_QG_DPP(CIR_QP_93, CIR_QP_4E, CIR_QP_39, CIR_M(K0), CIR_M(K1))           \
-  CIR_RD2(K0, K1)                                                             \
-  CIR_QG_DPP(CIR_QP_39, CIR_QP_4E, CIR_QP_93, CIR_M(K2), CIR_M(K3))           \
-  CIR_RD2(K2, K3)
-#define CIR_QCOMPRESS_RD                                                      \
-  CIR_QG_PLAIN(CIR_M(0), CIR_M(1)) CIR_RD2(0, 1)                              \
-  CIR_QG_DPP(CIR_QP_39, CIR_QP_4E, CIR_QP_93, CIR_M(2), CIR_M(3)) CIR_RD2(2, 3) \
-  CIR_QR_RD(4, 5, 6, 7) CIR_QR_RD(8, 9, 10, 11) CIR_QR_RD(12, 13, 14, 15)     \
-  CIR_QR_RD(16, 17, 18, 19) CIR_QR_RD(20, 21, 22, 23) CIR_QR_RD(24, 25, 26, 27) \
-  CIR_QR_RD(28, 29, 30, 31) CIR_QR_RD(32, 33, 34, 35) CIR_QR_RD(36, 37, 38, 39) \
-  CIR_QR(0, 1, 2, 3) CIR_QR(4, 5, 6, 7) "s_waitcnt lgkmcnt(0)\ns_nop 1\n"
 #define CIR_NO(k) [n##k] "=&v"(next[k])
 #define CIR_PA(k) [p##k] "v"(pa[k])
 
-__device__ __forceinline__ void compress_quad_asm_rd(uint64_t& a, uint64_t& b, uint64_t& c,
-                                                     uint64_t& d, const uint64_t (&m)[40],
-                                                     uint64_t (&next)[40],
-                                                     const uint32_t (&pa)[40]) {
-  uint64_t t, u;
-  asm volatile(CIR_QCOMPRESS_RD
-               : "+{v[40:41]}"(a), "+{v[42:43]}"(b), "+{v[44:45]}"(c), "+{v[46:47]}"(d),
-                 "=&{v[48:49]}"(t), "=&{v[50:51]}"(u), CIR_NO(0), CIR_NO(1), CIR_NO(2),
-                 CIR_NO(3), CIR_NO(4), CIR_NO(5), CIR_NO(6), CIR_NO(7), CIR_NO(8), CIR_NO(9),
-                 CIR_NO(10), CIR_NO(11), CIR_NO(12), CIR_NO(13), CIR_NO(14), CIR_NO(15),
-                 CIR_NO(16), CIR_NO(17), CIR_NO(18), CIR_NO(19), CIR_NO(20), CIR_NO(21),
-                 CIR_NO(22), CIR_NO(23), CIR_NO(24), CIR_NO(25), CIR_NO(26), CIR_NO(27),
-                 CIR_NO(28), CIR_NO(29), CIR_NO(30), CIR_NO(31), CIR_NO(32), CIR_NO(33),
-                 CIR_NO(34), CIR_NO(35), CIR_NO(36), CIR_NO(37), CIR_NO(38), CIR_NO(39)
+// One compression of the hand-scheduled quad loop (quad_fast in
+// kernels.hip), setup to finalisation in one block, so the compiler adds no
+// waits, moves or branches between compressions:
+//   d.lo = dv0.lo ^ (t & m0) (v_bitop3), a = h0, b = h1, c = cv, d.hi
+//   s_waitcnt vmcnt(2)      the line loaded two compressions ago has landed
+//   2 x ds_write_b128       that line (regs u/w) -> the quad's LDS line
+//   2 x global_load_dwordx4 a later line -> u/w, then ptr += step
+//   40 x ds_read_b64        the written line's message words -> next
+//   24 G steps              on the current words m
+//   finalisation            h0 ^= a ^ c[i+2]; h1 ^= b[i+3] ^ d[i+1] (DPP)
+//   s_waitcnt lgkmcnt(0)    next has landed (the reads ran under the G steps)
+// A wave alone issues ~1 instruction per 4 cycles whatever its kind
+// (tools/glue_ubench.hip), so the loop's cost is its instruction count.
+#define CIR_RD(k) "ds_read_b64 %[n" #k "], %[p" #k "]\n"
+#define CIR_RD40                                                              \
+  CIR_RD(0) CIR_RD(1) CIR_RD(2) CIR_RD(3) CIR_RD(4) CIR_RD(5) CIR_RD(6) CIR_RD(7) \
+  CIR_RD(8) CIR_RD(9) CIR_RD(10) CIR_RD(11) CIR_RD(12) CIR_RD(13) CIR_RD(14)  \
+  CIR_RD(15) CIR_RD(16) CIR_RD(17) CIR_RD(18) CIR_RD(19) CIR_RD(20) CIR_RD(21) \
+  CIR_RD(22) CIR_RD(23) CIR_RD(24) CIR_RD(25) CIR_RD(26) CIR_RD(27) CIR_RD(28) \
+  CIR_RD(29) CIR_RD(30) CIR_RD(31) CIR_RD(32) CIR_RD(33) CIR_RD(34) CIR_RD(35) \
+  CIR_RD(36) CIR_RD(37) CIR_RD(38) CIR_RD(39)
+#define CIR_QFAST                                                             \
+  CIR_QALIGN                                                                  \
+  "v_bitop3_b32 v46, %[dl], %[t], %[lm] bitop3:0x78\n"                        \
+  "v_mov_b32 v47, %[dh]\n"                                                    \
+  "s_waitcnt vmcnt(2)\n"                                                      \
+  "v_mov_b64 v[40:41], v[52:53]\n"                                            \
+  "v_mov_b64 v[42:43], v[54:55]\n"                                            \
+  "v_mov_b64_e64 v[44:45], %[cv]\n"                                           \
+  "ds_write_b128 %[wr], %[u]\n"                                               \
+  "ds_write_b128 %[wr], %[w] offset:16\n"                                     \
+  "global_load_dwordx4 %[u], %[ptr], off\n"                                   \
+  "global_load_dwordx4 %[w], %[ptr], off offset:16\n"                         \
+  "v_lshl_add_u64 %[ptr], %[ptr], 0, %[step]\n" CIR_RD40 CIR_QCOMPRESS        \
+  "v_xor_b32_dpp v48, v44, v40" CIR_QP_4E "\n"                                \
+  "v_xor_b32_dpp v49, v45, v41" CIR_QP_4E "\n"                                \
+  "v_xor_b32_dpp v54, v42, v54" CIR_QP_93 "\n"                                \
+  "v_xor_b32_dpp v55, v43, v55" CIR_QP_93 "\n"                                \
+  "v_xor_b32 v52, v52, v48\n"                                                 \
+  "v_xor_b32 v53, v53, v49\n"                                                 \
+  "v_xor_b32_dpp v54, v46, v54" CIR_QP_39 "\n"                                \
+  "v_xor_b32_dpp v55, v47, v55" CIR_QP_39 "\n"                                \
+  "s_waitcnt lgkmcnt(0)\n"
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // a VGPR quad for asm operands
+
+__device__ __forceinline__ void compress_quad_fast(uint64_t& h0, uint64_t& h1, uint64_t cv,
+                                                   uint32_t dl, uint32_t dh, uint32_t t,
+                                                   uint32_t m0, const uint64_t (&m)[40],
+                                                   uint64_t (&next)[40],
+                                                   const uint32_t (&pa)[40], uint32_t wr,
+                                                   u32x4& u, u32x4& w, const uint8_t*& ptr,
+                                                   uint64_t step) {
+  uint64_t a, b, c, d, x, y;
+  asm volatile(CIR_QFAST
+               : "+{v[52:53]}"(h0), "+{v[54:55]}"(h1), "=&{v[40:41]}"(a), "=&{v[42:43]}"(b),
+                 "=&{v[44:45]}"(c), "=&{v[46:47]}"(d), "=&{v[48:49]}"(x), "=&{v[50:51]}"(y),
+                 [u] "+v"(u), [w] "+v"(w), [ptr] "+v"(ptr), CIR_NO(0),
+                 CIR_NO(1), CIR_NO(2), CIR_NO(3), CIR_NO(4), CIR_NO(5), CIR_NO(6), CIR_NO(7),
+                 CIR_NO(8), CIR_NO(9), CIR_NO(10), CIR_NO(11), CIR_NO(12), CIR_NO(13),
+                 CIR_NO(14), CIR_NO(15), CIR_NO(16), CIR_NO(17), CIR_NO(18), CIR_NO(19),
+                 CIR_NO(20), CIR_NO(21), CIR_NO(22), CIR_NO(23), CIR_NO(24), CIR_NO(25),
+                 CIR_NO(26), CIR_NO(27), CIR_NO(28), CIR_NO(29), CIR_NO(30), CIR_NO(31),
+                 CIR_NO(32), CIR_NO(33), CIR_NO(34), CIR_NO(35), CIR_NO(36), CIR_NO(37),
+                 CIR_NO(38), CIR_NO(39)
                : CIR_MO(0), CIR_MO(1), CIR_MO(2), CIR_MO(3), CIR_MO(4), CIR_MO(5), CIR_MO(6),
                  CIR_MO(7), CIR_MO(8), CIR_MO(9), CIR_MO(10), CIR_MO(11), CIR_MO(12),
                  CIR_MO(13), CIR_MO(14), CIR_MO(15), CIR_MO(16), CIR_MO(17), CIR_MO(18),
@@ -635,7 +675,9 @@ __device__ __forceinline__ void compress_quad_asm_rd(uint64_t& a, uint64_t& b, u
                  CIR_PA(16), CIR_PA(17), CIR_PA(18), CIR_PA(19), CIR_PA(20), CIR_PA(21),
                  CIR_PA(22), CIR_PA(23), CIR_PA(24), CIR_PA(25), CIR_PA(26), CIR_PA(27),
                  CIR_PA(28), CIR_PA(29), CIR_PA(30), CIR_PA(31), CIR_PA(32), CIR_PA(33),
-                 CIR_PA(34), CIR_PA(35), CIR_PA(36), CIR_PA(37), CIR_PA(38), CIR_PA(39)
+                 CIR_PA(34), CIR_PA(35), CIR_PA(36), CIR_PA(37), CIR_PA(38), CIR_PA(39),
+                 [wr] "v"(wr), [cv] "v"(cv), [dl] "v"(dl), [dh] "v"(dh), [t] "s"(t),
+                 [lm] "v"(m0), [step] "s"(step)
                : "vcc", "memory");
 }
 
@@ -647,11 +689,11 @@ __device__ __forceinline__ void round_quad_asm(uint64_t& a, uint64_t& b, uint64_
                                                uint64_t x1, uint64_t y1) {
   uint64_t t, u;
   if constexpr (kFirst)
-    asm volatile(CIR_QG_PLAIN("%[x0]", "%[y0]") CIR_QG_DIAG CIR_QG_OPS);
+    asm volatile(CIR_QALIGN CIR_QG_PLAIN("%[x0]", "%[y0]") CIR_QG_DIAG CIR_QG_OPS);
   else if constexpr (kLast)
-    asm volatile(CIR_QG_COL CIR_QG_DIAG "s_nop 1\n" CIR_QG_OPS);
+    asm volatile(CIR_QALIGN CIR_QG_COL CIR_QG_DIAG "s_nop 1\n" CIR_QG_OPS);
   else
-    asm volatile(CIR_QG_COL CIR_QG_DIAG CIR_QG_OPS);
+    asm volatile(CIR_QALIGN CIR_QG_COL CIR_QG_DIAG CIR_QG_OPS);
 }
 
 // One compression of the chain owned by this quad.  line = the quad's 128-B
@@ -734,19 +776,6 @@ __device__ __forceinline__ void compress_quad_regs(uint64_t& h0, uint64_t& h1,
                                                    uint64_t dv) {
   uint64_t a = h0, b = h1, c = cv, d = dv;
   compress_quad_asm(a, b, c, d, m);
-  const uint64_t cc = mk64(qd<kQuadFromNext2>(lo32(c)) ^ lo32(a), qd<kQuadFromNext2>(hi32(c)) ^ hi32(a));
-  h0 = h0 ^ cc;
-  const uint64_t bb = mk64(qd<kQuadFromPrev>(lo32(b)) ^ lo32(h1), qd<kQuadFromPrev>(hi32(b)) ^ hi32(h1));
-  h1 = mk64(qd<kQuadFromNext>(lo32(d)) ^ lo32(bb), qd<kQuadFromNext>(hi32(d)) ^ hi32(bb));
-}
-
-__device__ __forceinline__ void compress_quad_regs_rd(uint64_t& h0, uint64_t& h1,
-                                                      const uint64_t (&m)[40],
-                                                      uint64_t (&next)[40],
-                                                      const uint32_t (&pa)[40], uint64_t cv,
-                                                      uint64_t dv) {
-  uint64_t a = h0, b = h1, c = cv, d = dv;
-  compress_quad_asm_rd(a, b, c, d, m, next, pa);
   const uint64_t cc = mk64(qd<kQuadFromNext2>(lo32(c)) ^ lo32(a), qd<kQuadFromNext2>(hi32(c)) ^ hi32(a));
   h0 = h0 ^ cc;
   const uint64_t bb = mk64(qd<kQuadFromPrev>(lo32(b)) ^ lo32(h1), qd<kQuadFromPrev>(hi32(b)) ^ hi32(h1));

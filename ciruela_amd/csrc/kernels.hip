@@ -35,16 +35,6 @@
 #define CIR_STR2(x) #x
 #define CIR_STR(x) CIR_STR2(x)
 
-// Quad mode with the next line's LDS reads inside the compression's asm
-// block (kRdi, compress_quad_asm_rd): per kernel, as measured
-// (profiles/r02/quad_rdi/).
-#ifndef CIR_QUAD_RDI_CHUNKS
-#define CIR_QUAD_RDI_CHUNKS 1
-#endif
-#ifndef CIR_QUAD_RDI_LONG
-#define CIR_QUAD_RDI_LONG 0
-#endif
-
 #ifndef CIR_QUAD_EXCLUSIVE
 #define CIR_QUAD_EXCLUSIVE 1
 #endif
@@ -55,7 +45,8 @@ namespace dev {
 static inline unsigned grid_for(uint64_t n, uint64_t per) { return (unsigned)((n + per - 1) / per); }
 
 #ifdef CIR_QUAD_CLOCK
-__device__ unsigned long long g_quad_clock[3];
+__device__ unsigned long long g_quad_clock[4];
+__device__ unsigned int g_quad_wave_ticks[16384];  // per wave: blockIdx * 4 + wave
 #endif
 
 // Pure uniform launch: nblk = gridDim.x * 256 equal blocks.
@@ -201,7 +192,7 @@ __device__ __forceinline__ void quad_init(uint32_t i, uint64_t& h0, uint64_t& h1
 // Advance a quad's chain over L bytes at p, t0 bytes already compressed.
 // final: the last line (partial, or the empty block of an empty input)
 // carries the final flag; otherwise L must be a multiple of 128.
-template <bool kPrefetchAll = false, bool kAsm = kQuadAsm, bool kRdi = false>
+template <bool kPrefetchAll = false, bool kAsm = kQuadAsm>
 __device__ __forceinline__ void quad_run(uint64_t& h0, uint64_t& h1, uint64_t t0,
                                          const uint8_t* p, uint32_t L, bool active, bool final,
                                          uint8_t* lds, const uint32_t (&addr)[48], uint32_t line,
@@ -239,43 +230,6 @@ __device__ __forceinline__ void quad_run(uint64_t& h0, uint64_t& h1, uint64_t t0
       const uint64_t dv = dv0 ^ (i == 0 ? t : 0ull) ^ ((i == 2 && last) ? ~0ull : 0ull);
       compress_quad_regs(h0, h1, m, cv, dv);
     };
-    if constexpr (kRdi) {
-      // The next line's 40 reads issue inside the compression's asm block
-      // (compress_quad_asm_rd), between its VALU instructions.
-      uint32_t pa[40];
-#pragma unroll
-      for (int k = 0; k < 40; ++k) pa[k] = (uint32_t)reinterpret_cast<uintptr_t>(lds) + addr[k];
-      auto put = [&](uint32_t it) {
-        *reinterpret_cast<uint4*>(lds + line + 32u * i) = u;
-        *reinterpret_cast<uint4*>(lds + line + 32u * i + 16u) = w;
-        if (it + 1 < total) fetch(it + 1, u, w);
-      };
-      auto step_rd = [&](uint32_t it, const uint64_t (&m)[40], uint64_t (&nx)[40]) {
-        const bool last = final && it + 1 == total;
-        const uint64_t t = t0 + (last ? (uint64_t)L : (uint64_t)(it + 1) * 128u);
-        const uint64_t dv = dv0 ^ (i == 0 ? t : 0ull) ^ ((i == 2 && last) ? ~0ull : 0ull);
-        compress_quad_regs_rd(h0, h1, m, nx, pa, cv, dv);
-      };
-      if (total) {
-        put(0);
-        quad_read_msg(ma, lds, addr);
-      }
-      for (uint32_t it = 0; it < total; it += 2) {
-        if (it + 1 >= total) {
-          step(it, ma);
-          break;
-        }
-        put(it + 1);
-        step_rd(it, ma, mb);
-        if (it + 2 >= total) {
-          step(it + 1, mb);
-          break;
-        }
-        put(it + 2);
-        step_rd(it + 1, mb, ma);
-      }
-      return;
-    }
     constexpr int kLgkm0 = 0xC07F;  // s_waitcnt lgkmcnt(0), vmcnt/expcnt untouched
     if (total) stage(0, ma);
     for (uint32_t it = 0; it < total; it += 2) {
@@ -304,7 +258,61 @@ __device__ __forceinline__ void quad_run(uint64_t& h0, uint64_t& h1, uint64_t t0
 
 // The chain of quad q of this wave (block b at p, L bytes; have = false for a
 // quad past the end) is hashed into out + 32 b.
-template <bool kPrefetchAll, bool kAsm = kQuadAsm, bool kRdi = false>
+// Hand-scheduled quad loop (compress_quad_fast): lines [0, nu) of this
+// quad's chain, nu even, >= 4 and wave-uniform, every line full, not final
+// and 16-B aligned for every active quad of the wave.  Line j+1 waits in
+// register set (j+1) % 2 until compression j writes it to LDS and reloads
+// the set with line min(j+3, nu-1) (clamped, so nothing past the uniform
+// part is read; the repeats are never used); compression j reads line j+1's
+// message words while it runs.  No branch, no compiler-inserted wait
+// between compressions.
+__device__ __forceinline__ void quad_fast(uint64_t& h0, uint64_t& h1, const uint8_t* p,
+                                          uint32_t nu, uint8_t* lds,
+                                          const uint32_t (&addr)[48], uint32_t line,
+                                          uint32_t i) {
+  const uint64_t cv = iv_lo(i), dv0 = iv_hi(i);
+  const uint32_t m0 = i == 0 ? ~0u : 0u;  // lane 0 of the quad carries t
+  const uint32_t base = (uint32_t)reinterpret_cast<uintptr_t>(lds);
+  uint32_t pa[40];
+#pragma unroll
+  for (int k = 0; k < 40; ++k) pa[k] = base + addr[k];
+  const uint32_t wr = base + line + 32u * i;
+  const uint8_t* src = p + 32u * i;
+  uint64_t ma[40], mb[40];
+  const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
+  *reinterpret_cast<u32x4*>(lds + line + 32u * i) = s4[0];
+  *reinterpret_cast<u32x4*>(lds + line + 32u * i + 16u) = s4[1];
+  quad_read_msg(ma, lds, addr);
+  u32x4 u1 = s4[8], w1 = s4[9], u0 = s4[16], w0 = s4[17];  // lines 1 and 2
+  // the compiler's own waits for these loads go here, not into the loop
+  asm volatile("" : "+v"(u1), "+v"(w1), "+v"(u0), "+v"(w0));
+  const uint8_t* ptr = src + 384;
+  const uint32_t dl = lo32(dv0), dh = hi32(dv0);
+  for (uint32_t j = 0; j < nu; j += 2) {
+    compress_quad_fast(h0, h1, cv, dl, dh, (j + 1u) * 128u, m0, ma, mb, pa, wr, u1, w1, ptr,
+                       j + 4u < nu ? 128u : 0u);
+    compress_quad_fast(h0, h1, cv, dl, dh, (j + 2u) * 128u, m0, mb, ma, pa, wr, u0, w0, ptr,
+                       j + 5u < nu ? 128u : 0u);
+  }
+  // the last loads are in flight into u0/w0/u1/w1: keep the registers until
+  // they have landed
+  asm volatile("s_waitcnt vmcnt(0)" ::"v"(u0), "v"(w0), "v"(u1), "v"(w1) : "memory");
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int s = 1; s < 64; s <<= 1) v = min(v, (uint32_t)__shfl_xor((int)v, s));
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
+// Lines of a quad's chain that quad_fast may take: full, not final, from a
+// 16-B aligned start (0 for an inactive quad of the wave: it does not run).
+#ifndef CIR_QUAD_FAST
+#define CIR_QUAD_FAST 1
+#endif
+constexpr uint32_t kQuadFastMin = 8;
+
+template <bool kPrefetchAll, bool kAsm = kQuadAsm>
 __device__ __forceinline__ void quad_chain(bool have, uint64_t b, const uint8_t* p, uint32_t L,
                                            uint8_t* __restrict__ out, uint8_t* lds,
                                            uint32_t wave_lds) {
@@ -314,7 +322,18 @@ __device__ __forceinline__ void quad_chain(bool have, uint64_t b, const uint8_t*
   quad_addr(addr, line, i);
   uint64_t h0, h1;
   quad_init(i, h0, h1);
-  quad_run<kPrefetchAll, kAsm, kRdi>(h0, h1, 0, p, have ? L : 0u, have, true, lds, addr, line, i);
+  uint32_t t0 = 0;
+  if constexpr (CIR_QUAD_FAST && kAsm && kPrefetchAll) {
+    const bool al16 = (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+    const uint32_t nf = !have ? 0xffffffffu : (al16 && L > 0u) ? (L - 1u) >> 7 : 0u;
+    const uint32_t nu = wave_min_u32(nf) & ~1u;
+    if (nu >= kQuadFastMin && nu != 0xfffffffeu) {
+      if (have) quad_fast(h0, h1, p, nu, lds, addr, line, i);
+      t0 = nu * 128u;
+    }
+  }
+  quad_run<kPrefetchAll, kAsm>(h0, h1, t0, p + t0, have ? L - t0 : 0u, have, true, lds, addr,
+                               line, i);
   if (have) *reinterpret_cast<uint64_t*>(out + b * 32u + 8u * i) = h0;
 }
 
@@ -334,7 +353,7 @@ __device__ __forceinline__ void quad_chains(const uint8_t* __restrict__ arena,
     o = off[b];
     L = len[b];
   }
-  quad_chain<kPrefetchAll, kAsm, CIR_QUAD_RDI_LONG != 0>(have, b, arena + o, L, out, lds, wave_lds);
+  quad_chain<kPrefetchAll, kAsm>(have, b, arena + o, L, out, lds, wave_lds);
 }
 
 // Hashes::hash_file split of one device-resident file, blocks [b0, nblk):
@@ -353,7 +372,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))
   const bool have = b < nblk;
   const uint64_t o = have ? b * bs : 0;
   const uint64_t rest = nbytes - o;
-  quad_chain<true, kQuadAsm, CIR_QUAD_RDI_CHUNKS != 0>(have, b, data + o, have ? (uint32_t)(rest < bs ? rest : bs) : 0u, out, lds,
+  quad_chain<true>(have, b, data + o, have ? (uint32_t)(rest < bs ? rest : bs) : 0u, out, lds,
                    wave * kQuadWaveLds);
 }
 
@@ -393,6 +412,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))
     atomicAdd(&g_quad_clock[0], (unsigned long long)(c1 - c0));
     atomicAdd(&g_quad_clock[1], (unsigned long long)(r1 - r0));
     atomicAdd(&g_quad_clock[2], 1ull);
+    atomicMax(&g_quad_clock[3], (unsigned long long)(r1 - r0));
+    if (blockIdx.x * 4 + wave < 16384) g_quad_wave_ticks[blockIdx.x * 4 + wave] = (unsigned)(r1 - r0);
   }
 #endif
 }
@@ -798,10 +819,14 @@ hipError_t launch_fill_splitmix64(uint64_t* p, uint64_t nwords, uint64_t seed,
 
 #ifdef CIR_QUAD_CLOCK
 // Diagnostics build only: sums of the quad waves' (shader cycles, 100 MHz
-// ticks, waves) since the last call; resets them.
-extern "C" int cir_debug_quad_clock(unsigned long long* out3) {
-  if (hipMemcpyFromSymbol(out3, HIP_SYMBOL(cir::dev::g_quad_clock), 24) != hipSuccess) return -1;
-  static const unsigned long long zero[3] = {0, 0, 0};
-  return hipMemcpyToSymbol(HIP_SYMBOL(cir::dev::g_quad_clock), zero, 24) == hipSuccess ? 0 : -1;
+// ticks, waves) and the longest wave's ticks since the last call; resets them.
+extern "C" int cir_debug_quad_clock(unsigned long long* out4) {
+  if (hipMemcpyFromSymbol(out4, HIP_SYMBOL(cir::dev::g_quad_clock), 32) != hipSuccess) return -1;
+  static const unsigned long long zero[4] = {0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(cir::dev::g_quad_clock), zero, 32) == hipSuccess ? 0 : -1;
+}
+extern "C" int cir_debug_quad_wave_ticks(unsigned* out, unsigned n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(cir::dev::g_quad_wave_ticks), 4ull * (n < 16384 ? n : 16384)) ==
+                 hipSuccess ? 0 : -1;
 }
 #endif

@@ -3,7 +3,7 @@ alone through a CIR_QUAD_CLOCK build (tools/build_variant.sh qclk
 -DCIR_QUAD_CLOCK=1) and prints each workload's step time, the quad waves'
 mean duration and their in-kernel shader clock (s_memtime / s_memrealtime).
 
-Usage: CIR_LANE_WG=N python tools/quad_clock.py abtest/qclk.so
+Usage: python tools/quad_clock.py abtest/qclk.so
 """
 import ctypes
 import os
@@ -35,11 +35,11 @@ def main():
     d_len = torch.from_numpy(lens).cuda()
     big = torch.nonzero(d_len >= (1 << 20)).flatten()
     work = {"cfg3": (d_off, d_len), "cfg3_1m_only": (d_off[big].contiguous(), d_len[big].contiguous())}
-    clk = (ctypes.c_ulonglong * 3)()
+    clk = (ctypes.c_ulonglong * 4)()
     for name, (o, ln) in work.items():
         n = ln.numel()
         out = torch.empty(32 * n, dtype=torch.uint8, device="cuda:0")
-        ts, ghz, wave_ms = [], [], []
+        ts, ghz, wave_ms, max_ms = [], [], [], []
         for rep in range(12):
             torch.cuda.synchronize()
             lib.cir_debug_quad_clock(clk)
@@ -56,9 +56,22 @@ def main():
             ts.append(e0.elapsed_time(e1))
             ghz.append(clk[0] / clk[1] * 0.1)
             wave_ms.append(clk[1] / clk[2] * 1e-5)
-        print("%-13s lane_wg=%-5s n=%7d step %.3f ms  quad wave %.3f ms  quad clock %.3f GHz" % (
-            name, os.environ.get("CIR_LANE_WG", "0"), n, statistics.median(ts),
-            statistics.median(wave_ms), statistics.median(ghz)), flush=True)
+            max_ms.append(clk[3] * 1e-5)
+        nw = (n + 15) // 16
+        ticks = (ctypes.c_uint * nw)()
+        if hasattr(lib, "cir_debug_quad_wave_ticks") and name.endswith("only"):
+            lib.cir_debug_quad_wave_ticks(ticks, nw)
+            by = {}
+            for w in range(nw - 1):  # the last wave may be partial
+                by.setdefault(("xcd", (w // 4) % 8), []).append(ticks[w] * 1e-5)
+                by.setdefault(("simd", w % 4), []).append(ticks[w] * 1e-5)
+            for k in sorted(by):
+                v = by[k]
+                print("   %s %d: waves %3d mean %.3f max %.3f min %.3f ms" % (
+                    k[0], k[1], len(v), sum(v) / len(v), max(v), min(v)))
+        print("%-13s n=%7d step %.3f ms  quad wave mean %.3f ms max %.3f ms  quad clock %.3f GHz" % (
+            name, n, statistics.median(ts), statistics.median(wave_ms), statistics.median(max_ms),
+            statistics.median(ghz)), flush=True)
 
 
 if __name__ == "__main__":
