@@ -449,10 +449,11 @@ __global__ void k_gate(const uint32_t* started, uint32_t target, uint32_t max_ro
 // set too high costs the leftover's time on the whole chip instead of
 // stretching the lane part past the quad part.  Config 3, one library, one
 // process per value (profiles/r02/lane_pacing/pace_sweep.log): pace 0 826
-// GiB/s, 40 863, 48 871, 52 877-887, 60 896, 80 878-880 (without the
-// helper, 56 fell to 771).
+// GiB/s, 40 863, 52 877-887, 60 896, 80 878-880 (without the helper, 56
+// fell to 771); with the hand-scheduled quad loop: 0 886-892, 48 952-957,
+// 60 948-957, 72 937-941, 90 907.
 #ifndef CIR_LANE_PACE
-#define CIR_LANE_PACE 60
+#define CIR_LANE_PACE 48
 #endif
 __global__ __launch_bounds__(kThreads, 4) void k_lane_rest(const uint8_t* __restrict__ arena,
                                                             const uint64_t* __restrict__ off,
