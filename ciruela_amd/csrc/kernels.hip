@@ -269,7 +269,7 @@ __device__ __forceinline__ void quad_run(uint64_t& h0, uint64_t& h1, uint64_t t0
 __device__ __forceinline__ void quad_fast(uint64_t& h0, uint64_t& h1, const uint8_t* p,
                                           uint32_t nu, uint8_t* lds,
                                           const uint32_t (&addr)[48], uint32_t line,
-                                          uint32_t i) {
+                                          uint32_t i, uint32_t t0 = 0) {
   const uint64_t cv = iv_lo(i), dv0 = iv_hi(i);
   const uint32_t m0 = i == 0 ? ~0u : 0u;  // lane 0 of the quad carries t
   const uint32_t base = (uint32_t)reinterpret_cast<uintptr_t>(lds);
@@ -289,10 +289,10 @@ __device__ __forceinline__ void quad_fast(uint64_t& h0, uint64_t& h1, const uint
   const uint8_t* ptr = src + 384;
   const uint32_t dl = lo32(dv0), dh = hi32(dv0);
   for (uint32_t j = 0; j < nu; j += 2) {
-    compress_quad_fast(h0, h1, cv, dl, dh, (j + 1u) * 128u, m0, ma, mb, pa, wr, u1, w1, ptr,
-                       j + 4u < nu ? 128u : 0u);
-    compress_quad_fast(h0, h1, cv, dl, dh, (j + 2u) * 128u, m0, mb, ma, pa, wr, u0, w0, ptr,
-                       j + 5u < nu ? 128u : 0u);
+    compress_quad_fast(h0, h1, cv, dl, dh, t0 + (j + 1u) * 128u, m0, ma, mb, pa, wr, u1, w1,
+                       ptr, j + 4u < nu ? 128u : 0u);
+    compress_quad_fast(h0, h1, cv, dl, dh, t0 + (j + 2u) * 128u, m0, mb, ma, pa, wr, u0, w0,
+                       ptr, j + 5u < nu ? 128u : 0u);
   }
   // the last loads are in flight into u0/w0/u1/w1: keep the registers until
   // they have landed
@@ -335,6 +335,29 @@ __device__ __forceinline__ void quad_chain(bool have, uint64_t b, const uint8_t*
   quad_run<kPrefetchAll, kAsm>(h0, h1, t0, p + t0, have ? L - t0 : 0u, have, true, lds, addr,
                                line, i);
   if (have) *reinterpret_cast<uint64_t*>(out + b * 32u + 8u * i) = h0;
+}
+
+// One quad's chain advanced over n bytes at p (t0 bytes already compressed;
+// final: the last line carries the final flag): the lines quad_fast can take
+// (16-B aligned, t stays below 2^32), then the general loop.  The index
+// footer (k_chain_step) and hash_bytes (k_single).
+__device__ __forceinline__ void quad_single(uint64_t& h0, uint64_t& h1, uint64_t t0,
+                                            const uint8_t* p, uint32_t n, bool final,
+                                            uint8_t* lds, const uint32_t (&addr)[48],
+                                            uint32_t i) {
+  uint32_t done = 0;
+  if constexpr (CIR_QUAD_FAST && kQuadAsm) {
+    const bool al16 = (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+    if (al16 && t0 + n < (1ull << 32)) {
+      const uint32_t nf = final ? (n > 0u ? (n - 1u) >> 7 : 0u) : n >> 7;
+      const uint32_t nu = nf & ~1u;
+      if (nu >= kQuadFastMin) {
+        quad_fast(h0, h1, p, nu, lds, addr, 0u, i, (uint32_t)t0);
+        done = nu * 128u;
+      }
+    }
+  }
+  quad_run<true>(h0, h1, t0 + done, p + done, n - done, true, final, lds, addr, 0u, i);
 }
 
 template <bool kPrefetchAll, bool kAsm>
@@ -500,7 +523,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const uint64_t t0 = st[8];
   uint64_t h0 = st[i], h1 = st[4 + i];
   if (t0 == 0 && st[9] == 0) quad_init(i, h0, h1);  // st[9] = 0: fresh state
-  quad_run<true>(h0, h1, t0, data, n, true, final != 0, lds, addr, 0u, i);
+  quad_single(h0, h1, t0, data, n, final != 0, lds, addr, i);
   st[i] = h0;
   st[4 + i] = h1;
   if (i == 0) {
@@ -554,7 +577,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
   quad_addr(addr, 0u, i);
   uint64_t h0, h1;
   quad_init(i, h0, h1);
-  quad_run<true>(h0, h1, 0, scratch, n, true, true, lds, addr, 0u, i);
+  quad_single(h0, h1, 0, scratch, n, true, lds, addr, i);
   reinterpret_cast<uint64_t*>(dout)[i] = h0;
 }
 
