@@ -44,6 +44,14 @@ namespace dev {
 
 static inline unsigned grid_for(uint64_t n, uint64_t per) { return (unsigned)((n + per - 1) / per); }
 
+uint64_t quad_small_batch() {
+  static const uint64_t v = [] {
+    const char* e = getenv("CIR_QUAD_SMALL_BATCH");
+    return e ? strtoull(e, nullptr, 10) : kQuadSmallBatch;
+  }();
+  return v;
+}
+
 #ifdef CIR_QUAD_CLOCK
 __device__ unsigned long long g_quad_clock[4];
 __device__ unsigned int g_quad_wave_ticks[16384];  // per wave: blockIdx * 4 + wave
@@ -701,12 +709,43 @@ hipError_t launch_uniform(Loader loader, const uint8_t* data, uint64_t bs, uint6
   return hipGetLastError();
 }
 
+// SIMDs of the current device (4 per CU), cached per device.
+static uint64_t device_simds() {
+  static uint64_t cache[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1024;
+  if (cache[dev] == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    cache[dev] = 4ull * (uint64_t)cus;
+  }
+  return cache[dev];
+}
+
+// Does a chunk-form file of nblk blocks run every block in quad mode?  Lane
+// mode holds 64 chains per wave, so its time steps with whole waves per SIMD:
+// a file of 1 < w <= 1.625 lane waves per SIMD costs as much as w = 2 on the
+// SIMDs that got two, while quad mode (16 chains per wave) grows smoothly.
+// Measured after the hand-scheduled quad loop (profiles/r02/crossover.log,
+// MI355X, 1024 SIMDs): 32 KiB x 81920 lane 1.94 ms / quad 1.67; x 98304
+// 1.95 / 1.94; x 65536 lane 1.16 / quad 1.34; x 131072 lane 2.14 / quad 2.50;
+// 256 KiB x 98304 lane 14.9 / quad 12.9.  Below 0.75 lane waves per SIMD
+// (the small-batch limit) quad mode always.
+static bool chunks_in_quad(uint64_t nblk, uint64_t bs) {
+  if (bs < 128ull * kQuadSmallMinLines || bs > 0xffffffffull) return false;
+  if (nblk < quad_small_batch()) return true;
+  const uint64_t wave_slots = 64ull * device_simds();  // one lane wave per SIMD
+  return nblk > wave_slots && nblk * 8 <= wave_slots * 13;
+}
+
 hipError_t launch_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint8_t* out,
                          hipStream_t s) {
   if (nbytes == 0) return hipSuccess;
   if (bs == 0) return hipErrorInvalidValue;
   const uint64_t nblk = (nbytes + bs - 1) / bs;
-  if (nblk < kQuadSmallBatch && bs >= 128ull * kQuadSmallMinLines && bs <= 0xffffffffull) {
+  if (chunks_in_quad(nblk, bs)) {
     hipLaunchKernelGGL(k_quad_chunks, dim3((unsigned)((nblk + 63) / 64)), dim3(kThreads), 0, s,
                        data, nbytes, bs, (uint64_t)0, nblk, out);
     return hipGetLastError();
@@ -739,7 +778,7 @@ hipError_t launch_chunks_split(const uint8_t* data, uint64_t nbytes, uint64_t bs
   const bool uni_ok = bs % 128u == 0 && (reinterpret_cast<uintptr_t>(data) & 15u) == 0 &&
                       bs / 128u <= 0xffffffffull && bs <= 0xffffffffull / 8u;
   const uint64_t grid = grid_for(grid_for(nfull, 64), kWaves);
-  if (!qs || qs == s || nblk < kQuadSmallBatch || !uni_ok || nfull == nblk ||
+  if (!qs || qs == s || chunks_in_quad(nblk, bs) || !uni_ok || nfull == nblk ||
       bs < 128ull * kQuadSmallMinLines || grid > 0x7fffffffull)
     return launch_chunks(data, nbytes, bs, out, s);
   hipError_t e = hipEventRecord(fork, s);
@@ -787,7 +826,7 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
     return v ? (uint32_t)strtoul(v, nullptr, 10) : (uint32_t)CIR_LANE_PACE;
   }();
   const uint32_t pace = aux != qs ? pace_env : 0u;  // only beside a concurrent quad part
-  const bool exclusive = CIR_QUAD_EXCLUSIVE && n >= kQuadSmallBatch;
+  const bool exclusive = CIR_QUAD_EXCLUSIVE && n >= quad_small_batch();
   hipError_t e = hipEventRecord(fork, s);
   if (e == hipSuccess && qs != s) e = hipStreamWaitEvent(qs, fork, 0);
   if (e == hipSuccess && aux != s) e = hipStreamWaitEvent(aux, fork, 0);

@@ -34,11 +34,14 @@ constexpr int kQuadMaxWg = 256;  // at most 256 x 64 = 16384 chains in quad mode
 #endif
 constexpr uint64_t kQuadSmallBatch = CIR_QUAD_SMALL_BATCH;
 constexpr uint32_t kQuadSmallMinLines = 8;
+// kQuadSmallBatch, or CIR_QUAD_SMALL_BATCH from the environment (read once;
+// a tuning probe for tools/ and the shape sweeps)
+uint64_t quad_small_batch();
 inline uint32_t quad_min_lines(uint64_t n) {
-  return n < kQuadSmallBatch ? kQuadSmallMinLines : kQuadMinLines;
+  return n < quad_small_batch() ? kQuadSmallMinLines : kQuadMinLines;
 }
 inline uint64_t quad_max_wg(uint64_t n) {
-  return n < kQuadSmallBatch ? (n + 63) / 64 : (uint64_t)kQuadMaxWg;
+  return n < quad_small_batch() ? (n + 63) / 64 : (uint64_t)kQuadMaxWg;
 }
 
 // nblk equal blocks of bs bytes at data (bs % 128 == 0, data 16-byte aligned,

@@ -118,6 +118,12 @@ def test_hash_bytes(gpu, oracle):
     # part (launch_chunks_split): 255 whole blocks, and whole + short ones
     (32768, 65535 * 32768),
     (1024, 65535 * 1024 + 3),
+    # 1 < lane waves per SIMD <= 1.625 (65537..106496 blocks on 1024 SIMDs):
+    # quad mode again (chunks_in_quad), whole and with a short tail
+    (1024, 81920 * 1024),
+    (1024, 81921 * 1024 + 500),
+    (2048, 106496 * 2048),
+    (1024, 106497 * 1024),           # just past the band: lane mode
 ])
 def test_chunks_dev_vs_oracle(gpu, ctx, oracle, bs, nbytes):
     import torch
