@@ -482,9 +482,10 @@ __global__ void k_gate(const uint32_t* started, uint32_t target, uint32_t max_ro
 // process per value (profiles/r02/lane_pacing/pace_sweep.log): pace 0 826
 // GiB/s, 40 863, 52 877-887, 60 896, 80 878-880 (without the helper, 56
 // fell to 771); with the hand-scheduled quad loop: 0 886-892, 48 952-957,
-// 60 948-957, 72 937-941, 90 907.
+// 60 948-957, 72 937-941, 90 907; after the ordering fixes: 0 908-918, 48
+// 977-993, 64 1012-1021, 80 970-973, 100 930-934.
 #ifndef CIR_LANE_PACE
-#define CIR_LANE_PACE 48
+#define CIR_LANE_PACE 64
 #endif
 __global__ __launch_bounds__(kThreads, 4) void k_lane_rest(const uint8_t* __restrict__ arena,
                                                             const uint64_t* __restrict__ off,
