@@ -266,6 +266,40 @@ def test_desc_paced_lane_part_single_workgroup(gpu, ctx, oracle):
     assert first_bad(out.cpu().numpy(), want) is None
 
 
+def test_desc_paced_lane_part_with_leftover(gpu, ctx, oracle):
+    """Lane pacing with more lane work than the paced workgroups finish: 64
+    chains of 1 MiB (the quad part) beside 60000 chains of ~64 KiB, ragged
+    (an exclusive batch; ~59 paced workgroups hold ~15 K chains at a time,
+    ~4 rounds of 512 compressions against the quad part's 8192), so the
+    helper k_lane_rest queued behind the quad part typically claims the
+    last tiles — every chain hashed exactly once either way."""
+    import torch
+    rng = random.Random(0x1EF7)
+    lens = [1 << 20] * 64 + [65536 - rng.randrange(0, 3) * 128 - rng.randrange(0, 2) * 5
+                             for _ in range(60000)]
+    rng.shuffle(lens)
+    offs, pos = [], 0
+    for ln in lens:
+        pos += (-pos) % 16
+        offs.append(pos)
+        pos += ln
+    data = dev_random(gpu, pos, seed=53)
+    d_off = torch.tensor(offs, dtype=torch.int64, device="cuda:0")
+    d_len = torch.tensor(lens, dtype=torch.int32, device="cuda:0")
+    out = torch.zeros(32 * len(lens), dtype=torch.uint8, device="cuda:0")
+    ctx.hash_blocks_dev(data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), len(lens),
+                        out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    host = data.cpu().numpy()
+    del data
+    ao = np.array(offs, dtype=np.uint64)
+    al = np.array(lens, dtype=np.uint32)
+    want = np.zeros(32 * len(lens), dtype=np.uint8)
+    oracle.oracle_hash_blocks(host.ctypes.data, ao.ctypes.data, al.ctypes.data, len(lens),
+                              want.ctypes.data, 16)
+    assert first_bad(out.cpu().numpy(), want) is None
+
+
 def test_desc_quad_capacity_overflow(gpu, ctx, oracle):
     """More long chains than the quad part holds (n_long > 64 x 256 = 16384
     chains of >= 128 KiB in a batch of >= 49153): the longest 16384 chains of
