@@ -602,8 +602,12 @@ hipError_t launch_single(const uint8_t* h_src, uint32_t n, uint8_t* d_scratch, u
 }
 
 // SHA-512/256 over a descriptor batch, one lane per block (dir-signature's
-// HashType::sha512_256()).
-__global__ __launch_bounds__(kThreads, 3) void k_sha_desc(const uint8_t* __restrict__ arena,
+// HashType::sha512_256()).  5 waves per SIMD: the asm rounds need 93 VGPRs
+// (the compiled ones 168, at 3 waves).
+#ifndef CIR_SHA_OCC
+#define CIR_SHA_OCC (CIR_SHA_ASM ? 5 : 3)
+#endif
+__global__ __launch_bounds__(kThreads, CIR_SHA_OCC) void k_sha_desc(const uint8_t* __restrict__ arena,
                                                            const uint64_t* __restrict__ off,
                                                            const uint32_t* __restrict__ len,
                                                            const uint32_t* __restrict__ perm,

@@ -8,6 +8,7 @@
 // v_lshl_add_u64, big-endian loads byte-swapped with v_perm_b32.
 #pragma once
 #include "blake2b_dev.hpp"
+#include "sha512_asm.h"
 
 namespace cir {
 namespace dev {
@@ -185,6 +186,32 @@ __device__ __forceinline__ void compress(uint64_t h[8], uint64_t w[16]) {
   h[7] += hh;
 }
 
+// The same compression as hand-scheduled asm (sha512_asm.h, generated by
+// tools/gen_sha_asm.py): the state and the 16-word schedule window pinned to
+// v[10:57], so renaming a..h between rounds costs nothing, 27 instructions
+// per round (46 with the schedule), round constants as SGPR operands.
+#ifndef CIR_SHA_ASM
+#define CIR_SHA_ASM 1
+#endif
+__device__ __forceinline__ void compress_asm(uint64_t h[8], uint64_t w[16]) {
+  uint64_t S[8], K[16];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) S[k] = h[k];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) K[k] = kK[k];
+  asm volatile(CIR_SHA_ROUNDS0 : CIR_SHA_STATE_OPS(S), CIR_SHA_W_OPS(w) : CIR_SHA_K_OPS(K)
+               : CIR_SHA_CLOBBERS);
+#pragma unroll 1
+  for (int t0 = 16; t0 < 80; t0 += 16) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) K[k] = kK[t0 + k];
+    asm volatile(CIR_SHA_ROUNDS1 : CIR_SHA_STATE_OPS(S), CIR_SHA_W_OPS(w) : CIR_SHA_K_OPS(K)
+                 : CIR_SHA_CLOBBERS);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) h[k] += S[k];
+}
+
 // Little-endian bytes of a padded block: the first n (0..128) message bytes,
 // 0x80 at byte n when pad80, zeros elsewhere.  Never reads past p + n.
 __device__ __forceinline__ void load_block_padded(uint64_t m[16], const uint8_t* p, uint32_t n,
@@ -250,7 +277,11 @@ __device__ __forceinline__ void chain(const uint8_t* p, uint64_t len, uint64_t h
       m[14] = len >> 61;
       m[15] = len << 3;
     }
+#if CIR_SHA_ASM
+    compress_asm(h, m);
+#else
     compress(h, m);
+#endif
   }
 }
 
