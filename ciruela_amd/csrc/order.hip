@@ -1,50 +1,80 @@
 // Processing order of a mixed-length descriptor batch (config 3).
 //
 // One lane hashes one block, so a wave costs as much as its longest chain.
-// Sorting descriptors by compression count (descending) puts chains of equal
+// Ordering descriptors by compression count (descending) puts chains of equal
 // length in the same waves and dispatches the longest ones first, so they
-// overlap with the short ones instead of trailing the launch.  The sort runs
-// on the device (hipCUB radix sort on 16-bit keys) inside the timed call.
+// overlap with the short ones instead of trailing the launch.  The order is
+// built on the device inside the timed call, by a counting sort over 4096
+// length bins in two kernels (plus one memset):
+//   k_chain_keys   bin of every chain, a per-workgroup LDS histogram added
+//                  into the global one, and the batch's counters;
+//   k_order_place  each workgroup scans the histogram (descending bins),
+//                  reserves its chunk's slots per bin with one atomic per
+//                  used bin, and places its chains through LDS cursors.
+// hipCUB's radix sort on 16-bit keys (CIR_ORDER_CUB=1) took ~10 launches:
+// ~0.13 ms with one context per process, ~0.5 ms with four (each launch
+// ~50 us once several contexts' streams share the hardware queues;
+// profiles/r02/early_quad/).
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 
 #include "kernels.hpp"
 
+#ifndef CIR_ORDER_CUB
+#define CIR_ORDER_CUB 0
+#endif
+
 namespace cir {
 namespace dev {
 
-constexpr int kKeyBits = 16;  // k_chain_keys' key width
+constexpr int kKeyBits = 16;  // the hipCUB path's key width
+constexpr uint32_t kBins = 4096;
+constexpr unsigned kOrderGrid = 512;  // workgroups of both kernels (at most)
 
-// Keys and the counters of a batch.  count[0] = long chains, count[2] = the
-// longest chain (compressions), count[4..5] = the lane part's work
-// (launch_mixed's pacing): compressions plus kLaneChainCost per chain for its
-// setup and digest store.  A bounded grid strides over the batch and each
-// workgroup adds its partial sums once: one atomic per wave and counter cost
-// ~0.36 ms at config 3's 986 K descriptors (15 K waves on three addresses).
-constexpr unsigned kKeyGridMax = 512;
+// Length bin, monotone in k (compressions): exact below 2048 (256 KiB, so
+// the quad thresholds of 8 and 1024 lines never share a bin with shorter
+// chains), then 128 bins per power of two up to 2^25 (< 0.8 % apart).
+__device__ __forceinline__ uint32_t length_bin(uint32_t k) {
+  if (k < 2048u) return k;
+  const uint32_t e = 31u - (uint32_t)__builtin_clz(k);  // 11 .. 25
+  return 2048u + (e - 11u) * 128u + ((k >> (e - 7u)) & 127u);
+}
 
+// Bins of a batch, the global histogram (hist, kBins counters) and the
+// batch's counters.  count[0] = long chains (>= min_lines lines), count[2] =
+// the longest chain (compressions), count[4..5] = the lane part's work
+// (launch_mixed's pacing): compressions plus kLaneChainCost per chain for
+// its setup and digest store.  A bounded grid strides over the batch and
+// each workgroup adds its partial sums once: one atomic per wave and
+// counter cost ~0.36 ms at config 3's 986 K descriptors (15 K waves on three
+// addresses).
 __global__ __launch_bounds__(256) void k_chain_keys(const uint32_t* __restrict__ len, uint64_t n,
                                                     uint32_t min_lines,
                                                     uint16_t* __restrict__ key,
                                                     uint32_t* __restrict__ idx,
-                                                    uint32_t* __restrict__ count) {
+                                                    uint32_t* __restrict__ count,
+                                                    uint32_t* __restrict__ hist) {
+  __shared__ uint32_t lh[kBins];
+  if (hist != nullptr)
+    for (uint32_t b = threadIdx.x; b < kBins; b += blockDim.x) lh[b] = 0;
+  __syncthreads();
   uint32_t nl = 0, mx = 0;
   uint64_t w = 0;
-  const uint32_t lane = threadIdx.x & 63u;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t l = len[i];
     const uint32_t k = l == 0 ? 1u : (l >> 7) + ((l & 127u) != 0);  // compressions, <= 2^25
-    // 16-bit sort key, monotone in k: exact below 32768 lines (4 MiB), then
-    // steps of 1024 lines (128 KiB) up to 2^25 lines.  With 2-byte keys
-    // rocPRIM sorts batches above 100 K items by onesweep (~4 launches);
-    // with 4-byte keys it chose block sort + merge sort up to 1 M items
-    // (~21 launches).  The launches, not the work, dominate the ordering:
-    // ~7 us each, ~45 us each with several contexts' queues in one process
-    // (profiles/r02/gtrace*).
-    key[i] = (uint16_t)(k < 32768u ? k : 32768u + ((k - 32768u) >> 10));
-    idx[i] = (uint32_t)i;
+    if (hist != nullptr) {
+      const uint32_t b = length_bin(k);
+      key[i] = (uint16_t)b;
+      atomicAdd(&lh[b], 1u);
+    } else {
+      // hipCUB path: 16-bit radix key, exact below 32768 lines, then steps
+      // of 1024 lines
+      key[i] = (uint16_t)(k < 32768u ? k : 32768u + ((k - 32768u) >> 10));
+      idx[i] = (uint32_t)i;
+    }
     if (k >= min_lines)
       ++nl;
     else
@@ -59,7 +89,7 @@ __global__ __launch_bounds__(256) void k_chain_keys(const uint32_t* __restrict__
   }
   __shared__ uint32_t s_nl[4], s_mx[4];
   __shared__ uint64_t s_w[4];
-  const uint32_t wave = threadIdx.x >> 6;
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   if (lane == 0) {
     s_nl[wave] = nl;
     s_mx[wave] = mx;
@@ -77,44 +107,122 @@ __global__ __launch_bounds__(256) void k_chain_keys(const uint32_t* __restrict__
     if (w) atomicAdd(reinterpret_cast<unsigned long long*>(count + 4), (unsigned long long)w);
     atomicMax(count + 2, mx);
   }
+  if (hist != nullptr)
+    for (uint32_t b = threadIdx.x; b < kBins; b += blockDim.x)
+      if (lh[b]) atomicAdd(&hist[b], lh[b]);
 }
 
+// Place chunk c = [c * C, min((c + 1) * C, n)) of the batch into perm in
+// descending bin order.  cursor: kBins zeroed counters (slots taken per bin).
+__global__ __launch_bounds__(256) void k_order_place(const uint16_t* __restrict__ key,
+                                                     uint64_t n, uint64_t chunk,
+                                                     const uint32_t* __restrict__ hist,
+                                                     uint32_t* __restrict__ cursor,
+                                                     uint32_t* __restrict__ perm) {
+  __shared__ uint32_t base[kBins];  // first slot of bin b: chains in bins above b
+  __shared__ uint32_t lc[kBins];    // this chunk's count per bin, then its cursors
+  __shared__ uint32_t part[256];
+  constexpr uint32_t kPer = kBins / 256;  // bins per thread in the scan
+  const uint32_t t = threadIdx.x;
+  // exclusive scan from the top bin down: thread t owns bins
+  // kBins-1-kPer*t .. kBins-kPer*(t+1)
+  uint32_t v[kPer], sum = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kPer; ++j) {
+    v[j] = hist[kBins - 1u - (kPer * t + j)];
+    sum += v[j];
+  }
+  part[t] = sum;
+  for (uint32_t b = t; b < kBins; b += 256) lc[b] = 0;
+  __syncthreads();
+  for (uint32_t s = 1; s < 256; s <<= 1) {  // inclusive scan of the partials
+    const uint32_t x = t >= s ? part[t - s] : 0u;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  uint32_t run = t ? part[t - 1] : 0u;
+#pragma unroll
+  for (uint32_t j = 0; j < kPer; ++j) {
+    base[kBins - 1u - (kPer * t + j)] = run;
+    run += v[j];
+  }
+  const uint64_t i0 = (uint64_t)blockIdx.x * chunk;
+  const uint64_t i1 = min(n, i0 + chunk);
+  for (uint64_t i = i0 + t; i < i1; i += 256) atomicAdd(&lc[key[i]], 1u);
+  __syncthreads();
+  // reserve this chunk's slots: one global atomic per bin it uses
+  for (uint32_t b = t; b < kBins; b += 256) {
+    const uint32_t c = lc[b];
+    if (c) base[b] += atomicAdd(&cursor[b], c);
+    lc[b] = 0;
+  }
+  __syncthreads();
+  for (uint64_t i = i0 + t; i < i1; i += 256) {
+    const uint32_t b = key[i];
+    perm[base[b] + atomicAdd(&lc[b], 1u)] = (uint32_t)i;
+  }
+}
+
+namespace {
+// scratch: [256 B counters][hist kBins x 4][cursor kBins x 4][key][perm]
+// (the hipCUB path: [key_in][key_out][idx_in][idx_out][temp])
+constexpr uint64_t kHead = 256 + 2ull * kBins * 4;
+}  // namespace
+
 size_t order_scratch_bytes(uint64_t n) {
+  const uint64_t arr = (n * 4 + 255) & ~(uint64_t)255;
+  if (!CIR_ORDER_CUB) return kHead + 2 * arr;
   size_t temp = 0;
   (void)hipcub::DeviceRadixSort::SortPairsDescending(nullptr, temp, (const uint16_t*)nullptr,
                                                      (uint16_t*)nullptr, (const uint32_t*)nullptr,
                                                      (uint32_t*)nullptr, (int)n, 0, kKeyBits);
-  return 256 + ((temp + 255) & ~(size_t)255) + 4 * ((n * 4 + 255) & ~(uint64_t)255);
+  return kHead + ((temp + 255) & ~(size_t)255) + 4 * arr;
 }
 
 hipError_t launch_order_desc(const uint32_t* len, uint64_t n, void* scratch, size_t bytes,
                              uint32_t** perm, uint32_t** n_long, hipStream_t s) {
   const uint64_t arr = (n * 4 + 255) & ~(uint64_t)255;
-  uint32_t* count = static_cast<uint32_t*>(scratch);
-  uint8_t* p = static_cast<uint8_t*>(scratch) + 256;
-  bytes -= 256;
+  uint8_t* base = static_cast<uint8_t*>(scratch);
+  uint32_t* count = reinterpret_cast<uint32_t*>(base);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(base + 256);
+  uint32_t* cursor = hist + kBins;
+  uint8_t* p = base + kHead;
   // count[0] = n_long; count[1] = quad workgroups started (launch_mixed's
   // gate); count[2] = longest chain; count[4..5] = lane work (k_chain_keys);
-  // count[6] = lane tiles claimed (k_lane_rest)
-  hipError_t e0 = hipMemsetAsync(count, 0, 32, s);
-  if (e0 != hipSuccess) return e0;
+  // count[6] = lane tiles claimed (k_lane_rest); then the histogram and the
+  // per-bin cursors: one memset for all of them
+  hipError_t e = hipMemsetAsync(count, 0, CIR_ORDER_CUB ? 32 : kHead, s);
+  if (e != hipSuccess) return e;
   *n_long = count;
-  uint16_t* key_in = reinterpret_cast<uint16_t*>(p);
+  const uint64_t kgrid = std::min<uint64_t>((n + 255) / 256, kOrderGrid);
+  uint16_t* key = reinterpret_cast<uint16_t*>(p);
+  if (!CIR_ORDER_CUB) {
+    uint32_t* out = reinterpret_cast<uint32_t*>(p + arr);
+    hipLaunchKernelGGL(k_chain_keys, dim3((unsigned)kgrid), dim3(256), 0, s, len, n,
+                       quad_min_lines(n), key, (uint32_t*)nullptr, count, hist);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const uint64_t chunk = (n + kgrid - 1) / kgrid;
+    hipLaunchKernelGGL(k_order_place, dim3((unsigned)kgrid), dim3(256), 0, s, key, n, chunk,
+                       hist, cursor, out);
+    *perm = out;
+    return hipGetLastError();
+  }
   uint16_t* key_out = reinterpret_cast<uint16_t*>(p + arr);
   uint32_t* idx_in = reinterpret_cast<uint32_t*>(p + 2 * arr);
   uint32_t* idx_out = reinterpret_cast<uint32_t*>(p + 3 * arr);
   void* temp = p + 4 * arr;
-  size_t temp_bytes = bytes - 4 * arr;
-  const uint64_t kgrid = std::min<uint64_t>((n + 255) / 256, kKeyGridMax);
+  size_t temp_bytes = bytes - kHead - 4 * arr;
   hipLaunchKernelGGL(k_chain_keys, dim3((unsigned)kgrid), dim3(256), 0, s, len, n,
-                     quad_min_lines(n), key_in, idx_in, count);
-  hipError_t e = hipGetLastError();
+                     quad_min_lines(n), key, idx_in, count, (uint32_t*)nullptr);
+  e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (n == 1) {  // one chain (hash_bytes, an index footer): nothing to order
     *perm = idx_in;
     return hipSuccess;
   }
-  e = hipcub::DeviceRadixSort::SortPairsDescending(temp, temp_bytes, key_in, key_out, idx_in,
+  e = hipcub::DeviceRadixSort::SortPairsDescending(temp, temp_bytes, key, key_out, idx_in,
                                                    idx_out, (int)n, 0, kKeyBits, s);
   *perm = idx_out;
   return e;
