@@ -475,7 +475,7 @@ __global__ void k_gate(const uint32_t* started, uint32_t target, uint32_t max_ro
 // lane work (count[4..5]) within the longest quad chain (count[2]) at `pace`
 // lane compressions per workgroup per quad compression; the other
 // workgroups exit at once.  Waves claim tiles of 64 chains of the order from
-// count[6], so a helper launch of this kernel behind the quad part (pace 0)
+// count[6], so a helper launch behind the quad part (k_lane_tiles, helper)
 // finishes whatever the paced part left when the quad part ended: a pace
 // set too high costs the leftover's time on the whole chip instead of
 // stretching the lane part past the quad part.  Config 3, one library, one
@@ -487,20 +487,60 @@ __global__ void k_gate(const uint32_t* started, uint32_t target, uint32_t max_ro
 #ifndef CIR_LANE_PACE
 #define CIR_LANE_PACE 64
 #endif
+
+// Workgroups of a paced lane part, or 0 when the batch is not paced (no
+// pacing asked, no long chain, or more long chains than the quad part holds).
+__device__ __forceinline__ uint64_t lane_paced_wgs(const uint32_t* count, uint32_t nq_wg,
+                                                    uint32_t pace) {
+  const uint32_t nlong = count[0];
+  if (pace == 0 || nlong == 0 || nlong > nq_wg * 64u) return 0;
+  const uint64_t lq = (uint64_t)count[2] * pace;
+  const uint64_t work = *reinterpret_cast<const unsigned long long*>(count + 4);
+  return max<uint64_t>(1, (work + lq - 1) / lq);
+}
+
+__device__ __forceinline__ void lane_chain(const uint8_t* __restrict__ arena,
+                                           const uint64_t* __restrict__ off,
+                                           const uint32_t* __restrict__ len, uint32_t b,
+                                           uint8_t* __restrict__ out) {
+  uint64_t h[8];
+  hash_chain(arena + off[b], len[b], h);
+  store_digest(out + (uint64_t)b * 32u, h);
+}
+
+// Unpaced lane part: one lane per chain, one pass (100 VGPRs, 5 waves per
+// SIMD).  With pace != 0 it leaves a paced batch to k_lane_tiles.
 __global__ __launch_bounds__(kThreads, 4) void k_lane_rest(const uint8_t* __restrict__ arena,
                                                             const uint64_t* __restrict__ off,
                                                             const uint32_t* __restrict__ len,
                                                             const uint32_t* __restrict__ perm,
-                                                            uint64_t n, uint32_t* count,
+                                                            uint64_t n, const uint32_t* count,
                                                             uint32_t nq_wg, uint32_t pace,
                                                             uint8_t* __restrict__ out) {
-  const uint32_t nlong = count[0];
-  const uint32_t nl = min(nlong, nq_wg * 64u);
-  if (pace != 0 && nlong > 0 && nlong <= nq_wg * 64u) {
-    const uint64_t lq = (uint64_t)count[2] * pace;
-    const uint64_t work = *reinterpret_cast<const unsigned long long*>(count + 4);
-    if (blockIdx.x >= max<uint64_t>(1, (work + lq - 1) / lq)) return;
-  }
+  if (lane_paced_wgs(count, nq_wg, pace) != 0) return;
+  const uint32_t nl = min(count[0], nq_wg * 64u);
+  const uint64_t j = nl + (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (j < n) lane_chain(arena, off, len, perm[j], out);
+}
+
+// Paced lane part (helper == 0): only lane_paced_wgs() workgroups run, and
+// waves claim tiles of 64 chains of the order from count[6]; the helper
+// (helper == 1, queued behind the quad part on its stream) claims whatever
+// the paced part left when the quad part ended, with the whole grid.  Both
+// leave an unpaced batch to k_lane_rest.  The tile loop costs registers
+// (120 VGPRs, 4 waves per SIMD): a lane-only batch through it ran 5.3 ms
+// instead of 3.9.
+__global__ __launch_bounds__(kThreads, 4) void k_lane_tiles(const uint8_t* __restrict__ arena,
+                                                             const uint64_t* __restrict__ off,
+                                                             const uint32_t* __restrict__ len,
+                                                             const uint32_t* __restrict__ perm,
+                                                             uint64_t n, uint32_t* count,
+                                                             uint32_t nq_wg, uint32_t pace,
+                                                             uint32_t helper,
+                                                             uint8_t* __restrict__ out) {
+  const uint64_t active = lane_paced_wgs(count, nq_wg, pace);
+  if (active == 0 || (!helper && blockIdx.x >= active)) return;
+  const uint32_t nl = count[0];  // every long chain is in the quad part
   // nothing left (the helper behind a paced part that finished): leave
   // without touching the tile counter, so thousands of idle waves do not
   // queue their atomics on one address (~0.18 ms at config 3)
@@ -514,12 +554,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_lane_rest(const uint8_t* __rest
     const uint64_t j0 = nl + (uint64_t)t * 64u;
     if (j0 >= n) break;
     const uint64_t j = j0 + lane;
-    if (j < n) {
-      const uint32_t b = perm[j];
-      uint64_t h[8];
-      hash_chain(arena + off[b], len[b], h);
-      store_digest(out + (uint64_t)b * 32u, h);
-    }
+    if (j < n) lane_chain(arena, off, len, perm[j], out);
   }
 }
 
@@ -857,13 +892,19 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
     hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, aux, n_long + 1, (uint32_t)nq, 600u);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
+    // unpaced batches: k_lane_rest; paced ones: k_lane_tiles (each leaves
+    // the other case at once), and the helper behind the quad part
     hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads), 0, aux, arena, off,
                        len, perm, n, n_long, (uint32_t)nq, pace, out);
-    if (pace != 0) {  // helper behind the quad part: the paced part's leftover
+    if (pace != 0) {
       e = hipGetLastError();
       if (e != hipSuccess) return e;
-      hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads), 0, qs, arena,
-                         off, len, perm, n, n_long, (uint32_t)nq, 0u, out);
+      hipLaunchKernelGGL(k_lane_tiles, dim3((unsigned)lane_grid), dim3(kThreads), 0, aux, arena,
+                         off, len, perm, n, n_long, (uint32_t)nq, pace, 0u, out);
+      e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(k_lane_tiles, dim3((unsigned)lane_grid), dim3(kThreads), 0, qs, arena,
+                         off, len, perm, n, n_long, (uint32_t)nq, pace, 1u, out);
     }
   } else {
     hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads), 0, aux, arena, off,
