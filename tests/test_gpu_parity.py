@@ -575,6 +575,59 @@ def test_check_file_commit(gpu, small_ctx, tmp_path):
         assert gpu.Hashes(b"", 32768).check_file(f, context=small_ctx)
 
 
+@pytest.mark.parametrize("aligned", [True, False])
+def test_desc_quad_fast_loop_edges(gpu, ctx, oracle, aligned):
+    """The hand-scheduled quad loop (quad_fast) at its edges: a small batch
+    (every chain of >= 8 lines in quad mode) whose waves mix chains of 8..40
+    lines, exact multiples of 128 (the last full line is the final one) and
+    ragged tails, so the wave-uniform count nu lands on 0, 6, 8 (the loop's
+    minimum) and above, with the rest of each chain in the general loop;
+    with misaligned starts every wave falls back to the general loop."""
+    import torch
+    rng = random.Random(0xFA57 + aligned)
+    lens = []
+    for _ in range(900):
+        lines = rng.randrange(8, 41)
+        lens.append(lines * 128 - rng.choice([0, 0, 1, 64, 127]))
+    lens += [9 * 128, 9 * 128 + 1, 10 * 128, 8 * 128, 8 * 128 + 1, 17 * 128 - 1]
+    rng.shuffle(lens)
+    offs, pos = [], 0
+    for i, ln in enumerate(lens):
+        pos += (-pos) % 16 + (0 if aligned else (i % 7) + 1)
+        offs.append(pos)
+        pos += ln
+    data = dev_random(gpu, pos, seed=61 + aligned)
+    d_off = torch.tensor(offs, dtype=torch.int64, device="cuda:0")
+    d_len = torch.tensor(lens, dtype=torch.int32, device="cuda:0")
+    out = torch.zeros(32 * len(lens), dtype=torch.uint8, device="cuda:0")
+    ctx.hash_blocks_dev(data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), len(lens),
+                        out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    host = data.cpu().numpy()
+    want = np.zeros(32 * len(lens), dtype=np.uint8)
+    ao = np.array(offs, dtype=np.uint64)
+    al = np.array(lens, dtype=np.uint32)
+    oracle.oracle_hash_blocks(host.ctypes.data, ao.ctypes.data, al.ctypes.data, len(lens),
+                              want.ctypes.data, 8)
+    assert first_bad(out.cpu().numpy(), want) is None
+
+
+@pytest.mark.parametrize("bs", [8 * 128, 9 * 128, 10 * 128 + 5, 4096])
+def test_chunks_quad_fast_loop_block_sizes(gpu, ctx, oracle, bs):
+    """Chunk-form files in quad mode with blocks of 8 / 9 / 10+ lines: the
+    fast loop's count nu is 6 (loop skipped), 8 (its minimum) and 10, plus
+    a short last block."""
+    import torch
+    nbytes = 3000 * bs + 333
+    data = dev_random(gpu, nbytes, seed=bs)
+    nb = (nbytes + bs - 1) // bs
+    out = torch.zeros(nb * 32, dtype=torch.uint8, device="cuda:0")
+    ctx.hash_chunks_dev(data.data_ptr(), nbytes, bs, out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    want = oracle_chunks(oracle, data.cpu().numpy(), nbytes, bs)
+    assert first_bad(out.cpu().numpy(), want) is None
+
+
 def test_desc_quad_mode_edges(gpu, ctx, oracle):
     """Chains around the quad-mode threshold (1024 lines = 128 KiB) and long
     ragged chains: 37 long chains (a partial 16-chain wave), misaligned and
