@@ -26,6 +26,7 @@
 #include "kernels.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 
 #include "blake2b_dev.hpp"
@@ -280,6 +281,9 @@ __device__ __forceinline__ void quad_fast(uint64_t& h0, uint64_t& h1, const uint
                                           uint32_t i, uint32_t t0 = 0) {
   const uint64_t cv = iv_lo(i), dv0 = iv_hi(i);
   const uint32_t m0 = i == 0 ? ~0u : 0u;  // lane 0 of the quad carries t
+  // LDS byte address of the kernel's shared array: a generic pointer into
+  // LDS is the shared aperture's base in its high half and the LDS offset in
+  // its low half, so the low 32 bits are what ds_read / ds_write take
   const uint32_t base = (uint32_t)reinterpret_cast<uintptr_t>(lds);
   uint32_t pa[40];
 #pragma unroll
@@ -754,19 +758,22 @@ hipError_t launch_uniform(Loader loader, const uint8_t* data, uint64_t bs, uint6
   return hipGetLastError();
 }
 
-// SIMDs of the current device (4 per CU), cached per device.
+// SIMDs of the current device (4 per CU), cached per device (several host
+// threads may ask at once: the cache slots are atomic).
 static uint64_t device_simds() {
-  static uint64_t cache[64] = {};
+  static std::atomic<uint64_t> cache[64];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1024;
-  if (cache[dev] == 0) {
+  uint64_t v = cache[dev].load(std::memory_order_relaxed);
+  if (v == 0) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         cus <= 0)
       cus = 256;
-    cache[dev] = 4ull * (uint64_t)cus;
+    v = 4ull * (uint64_t)cus;
+    cache[dev].store(v, std::memory_order_relaxed);
   }
-  return cache[dev];
+  return v;
 }
 
 // Does a chunk-form file of nblk blocks run every block in quad mode?  Lane
