@@ -263,7 +263,7 @@ bool parse(const uint8_t* data, size_t len, Index* out, std::string* err) {
         return false;
       }
       const uint64_t bs = out->header.block_size;
-      const uint64_t want = (e.size + bs - 1) / bs;
+      const uint64_t want = e.size / bs + (e.size % bs != 0);  // no wrap near 2^64
       if (tok.size() - 3 != want) {
         *err = "wrong number of hashes on line " + std::to_string(li + 1);
         return false;
@@ -273,6 +273,12 @@ bool parse(const uint8_t* data, size_t len, Index* out, std::string* err) {
       for (size_t k = 3; k < tok.size(); ++k) {
         if (!from_hex(tok[k], &one)) {
           *err = "bad hash hex on line " + std::to_string(li + 1);
+          return false;
+        }
+        if (one.size() != dl) {  // the hashes are stored back to back
+          out->bad_hash_size = true;
+          *err = "hash of " + std::to_string(one.size()) + " bytes on line " +
+                 std::to_string(li + 1);
           return false;
         }
         e.hashes.insert(e.hashes.end(), one.begin(), one.end());

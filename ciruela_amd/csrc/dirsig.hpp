@@ -73,6 +73,11 @@ struct Index {
   Header header;
   std::vector<Entry> entries;
   std::vector<uint8_t> footer;  // decoded last line
+  // set (and parse() fails) when a block hash decodes to other than
+  // digest_len bytes: register_dir reports it as DirError::HashSize
+  // (BlockHash::from_bytes, src/blocks.rs:168-170), other callers as a
+  // parse error
+  bool bad_hash_size = false;
 };
 
 // Parse a whole index.  Returns false with *err set on malformed input

@@ -111,7 +111,9 @@ int cir_blocks_register_dir(cir_blocks* h, const char* dir, const uint8_t* index
   if (!h || !dir || !index) return fail(CIR_EINVAL, "null pointer");
   dirsig::Index idx;
   std::string err;
-  if (!dirsig::parse(index, len, &idx, &err)) return fail(CIR_EPARSE, "error parsing index: " + err);
+  if (!dirsig::parse(index, len, &idx, &err))
+    return idx.bad_hash_size ? fail(CIR_EHASHSIZE, "hash size is unsupported: " + err)
+                             : fail(CIR_EPARSE, "error parsing index: " + err);
   const uint64_t bs = idx.header.block_size;
   const size_t dl = dirsig::digest_len(idx.header.hash);
   if (dl != 32) return fail(CIR_EHASHSIZE, "hash size is unsupported");

@@ -129,6 +129,31 @@ def test_register_dir_errors(tmp_path):
                                       b"  f f 5000 " + b"ab" * 32 + b"\n" + b"ab" * 32 + b"\n")
 
 
+def test_register_dir_hash_size_and_huge_size(tmp_path):
+    """A block hash that is not 32 bytes is DirError::HashSize
+    (BlockHash::from_bytes, src/blocks.rs:168-170), not a silently
+    mis-split hash list; the rewrite reports it as a parse error.  A size
+    near 2^64 needs its full hash count (no wrap in ceil(size / bs))."""
+    import ctypes
+    r = ca.ThreadedBlockReader()
+    short = (b"DIRSIGNATURE.v1 blake2b/256 block_size=4096\n/\n  f f 10 " + b"ab" * 16 +
+             b"\n" + b"ab" * 32 + b"\n")
+    with pytest.raises(ca.DirError) as e:
+        r.register_dir(str(tmp_path), short)
+    assert e.value.status == _native.CIR_EHASHSIZE
+    out, ln = ctypes.c_void_p(), ctypes.c_size_t()
+    rc = _native.lib.cir_index_rewrite(None, short, len(short), ctypes.byref(out),
+                                       ctypes.byref(ln))
+    assert rc == _native.CIR_EPARSE
+    huge = (b"DIRSIGNATURE.v1 blake2b/256 block_size=32768\n/\n  f f 18446744073709551615\n" +
+            b"ab" * 32 + b"\n")
+    with pytest.raises(ca.DirError) as e:
+        r.register_dir(str(tmp_path), huge)
+    assert e.value.status == _native.CIR_EPARSE
+    assert b"wrong number of hashes" in _native.lib.cir_last_error()
+    assert len(r) == 0
+
+
 def test_block_hash_type():
     h = ca.BlockHash(bytes(range(32)))
     assert str(h) == bytes(range(32)).hex()
