@@ -850,8 +850,24 @@ def test_randomized_batches_and_files(gpu, ctx, oracle, seed):
     quad thresholds (8 and 1024 lines), misaligned offsets; device-resident
     files with random block sizes (multiples of 128 or not) and block counts
     on both sides of the limit."""
+    random_case(gpu, ctx, oracle, 1000 + seed)
+
+
+def test_randomized_sweep(gpu, ctx, oracle):
+    """The same random cases over CIR_SWEEP_SEEDS more seeds (0 = skipped;
+    a long parity sweep run by hand, profiles/r02/parity_sweep/)."""
+    n = int(os.environ.get("CIR_SWEEP_SEEDS", "0"))
+    if n == 0:
+        pytest.skip("set CIR_SWEEP_SEEDS to run the sweep")
+    first = int(os.environ.get("CIR_SWEEP_FIRST", "5000"))
+    for s in range(first, first + n):
+        random_case(gpu, ctx, oracle, s)
+        print("seed %d ok" % s, flush=True)
+
+
+def random_case(gpu, ctx, oracle, seed):
     import torch
-    rng = random.Random(1000 + seed)
+    rng = random.Random(seed)
     # descriptor batch
     n = rng.choice([1, 7, 300, 5000, 49152, 49153, 60000])
     lens = []
@@ -896,6 +912,26 @@ def test_randomized_batches_and_files(gpu, ctx, oracle, seed):
     torch.cuda.synchronize()
     fh = fdata.cpu().numpy()[skew:].copy()
     assert first_bad(fout.cpu().numpy(), oracle_chunks(oracle, fh, nbytes, bs)) is None
+    del fdata, fout
+    # SHA-512/256 descriptors (k_sha_desc), a smaller batch
+    n = rng.choice([1, 3, 200, 3000])
+    lens = [rng.choice([0, 1, 111, 112, 127, 128, 129, 239, 240, 4096, 32768,
+                        rng.randrange(0, 300000)]) for _ in range(n)]
+    offs, pos = [], 0
+    for ln in lens:
+        pos += rng.randrange(0, 9)
+        offs.append(pos)
+        pos += ln
+    data = dev_random(gpu, max(pos, 1), seed=31 + seed)
+    d_off = torch.tensor(offs, dtype=torch.int64, device="cuda:0")
+    d_len = torch.tensor(lens, dtype=torch.int32, device="cuda:0")
+    out = torch.zeros(32 * n, dtype=torch.uint8, device="cuda:0")
+    ctx.hash_blocks_dev(data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, out.data_ptr(), 0,
+                        hash_type=gpu.HashType.sha512_256())
+    torch.cuda.synchronize()
+    host = data.cpu().numpy().tobytes()
+    want = b"".join(oracle_sha(oracle, host[o:o + ln]) for o, ln in zip(offs, lens))
+    assert first_bad(out.cpu().numpy(), np.frombuffer(want, dtype=np.uint8)) is None
 
 
 def test_reference_hidden_line_on_gpu(gpu, small_ctx, tmp_path, dirsig_example):
