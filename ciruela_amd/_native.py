@@ -102,6 +102,7 @@ _SIGS = {
     "cir_check_file": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, c_vp,
                                       ctypes.c_size_t, ctypes.POINTER(ctypes.c_int)]),
     "cir_debug_compress_only_dev": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, c_vp, c_vp]),
+    "cir_debug_relay_blocks": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint64]),
     "cir_debug_hash_uniform_dev": (ctypes.c_int, [ctypes.c_int, c_vp, ctypes.c_uint64,
                                                   ctypes.c_uint64, c_vp, c_vp]),
     "cir_fill_splitmix64_dev": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint64,

@@ -395,6 +395,9 @@ __device__ __forceinline__ void quad_chains(const uint8_t* __restrict__ arena,
 // every block in quad mode (16 per wave).  The whole file when it has fewer
 // than kQuadSmallBatch blocks; otherwise the ragged rest beside k_chunks'
 // uniform part (launch_chunks_split).
+// kBase: the base part beside a relay (launch_chunks_split) runs at priority
+// 2, so the relay's segments (priority 3) issue first on a shared SIMD.
+template <bool kBase = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_quad_chunks(
     const uint8_t* __restrict__ data, uint64_t nbytes, uint64_t bs, uint64_t b0, uint64_t nblk,
     uint8_t* __restrict__ out) {
@@ -402,13 +405,177 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t first = b0 + ((uint64_t)blockIdx.x * kWaves + wave) * 16u;
   if (first >= nblk) return;
-  __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(kBase ? 2 : 3);
   const uint64_t b = first + ((threadIdx.x & 63u) >> 2);
   const bool have = b < nblk;
   const uint64_t o = have ? b * bs : 0;
   const uint64_t rest = nbytes - o;
   quad_chain<true>(have, b, data + o, have ? (uint32_t)(rest < bs ? rest : bs) : 0u, out, lds,
                    wave * kQuadWaveLds);
+}
+
+// ---------------------------------------------------------------------------
+// Relay: the whole blocks of a file beyond k whole lane waves per SIMD.
+// Lane mode holds 64 chains per wave, so a file of 65536 k + E blocks (E
+// small, 1024 SIMDs) costs k + 1 lane waves on the SIMDs that get the extra
+// chains: 65537 x 32 KiB ran 1.51 ms against 1.16 ms for 65536.  Instead the
+// first 65536 k blocks run in lane mode (k_chunks) and the E extra chains in
+// quad mode, 16 per group (one wave), each chain cut into segments of
+// seg_lines lines that run one after another in different workgroups: a
+// segment's wave waits for its predecessor's flag, picks the chain values up
+// from `state`, compresses its lines at s_setprio 3 and hands on.  The extra
+// work is spread thin over many SIMDs instead of doubling a few of them.
+// Workgroup x = segment x / ngroups of group x % ngroups, so segments are
+// dispatched in order and a waiting wave's predecessor is always resident
+// or done.  A wave that waits longer than max_polls polls leaves its segment
+// (and every later one) to k_quad_relay_finish, queued behind on the same
+// stream, so the relay always drains and the digests never depend on timing.
+// flags[g] = segments of group g done (zeroed before the launch).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kRelayGroupChains = 16;
+#ifndef CIR_RELAY_SLEEP
+#define CIR_RELAY_SLEEP 8  // s_sleep units (64 clocks): ~0.25 us between polls
+#endif
+// Each segment adds its lines' quad-mode work (~1 us per line) to the lane
+// wave of the SIMD it lands on, so short chains take short segments: at
+// 32 lines, 16-line segments cost the lane part 12 %.  8 = the hand-
+// scheduled loop's minimum (kQuadFastMin).  Beside quad-mode base waves the
+// relayed chain is as long as the base's and every hand-off (~2-4 us) adds
+// to it, so segments there are 16 lines or more.
+constexpr uint32_t kRelayMinSegLines = 8;
+
+// Lines [l0, l1) of a chain of full 128-B lines at blk (16-B aligned);
+// final: l1 is the chain's last line.  nu is wave-uniform because every chain
+// of the wave has the same lines.
+__device__ __forceinline__ void quad_lines(uint64_t& h0, uint64_t& h1, const uint8_t* blk,
+                                           uint32_t l0, uint32_t l1, bool final, bool have,
+                                           uint8_t* lds, const uint32_t (&addr)[48],
+                                           uint32_t line, uint32_t i) {
+  const uint32_t n = l1 - l0;
+  uint32_t done = 0;
+  if constexpr (CIR_QUAD_FAST && kQuadAsm) {
+    const uint32_t nu = (final ? n - 1u : n) & ~1u;
+    if (nu >= kQuadFastMin) {
+      if (have) quad_fast(h0, h1, blk + (uint64_t)l0 * 128u, nu, lds, addr, line, i, l0 * 128u);
+      done = nu;
+    }
+  }
+  quad_run<true>(h0, h1, (uint64_t)(l0 + done) * 128u, blk + (uint64_t)(l0 + done) * 128u,
+                 have ? (n - done) * 128u : 0u, have, final, lds, addr, line, i);
+}
+
+// This lane's index in the wave, recomputed where it is called (volatile: the
+// compiler may not keep it, or anything derived from it, live in a VGPR
+// across the compression loop instead).
+__device__ __forceinline__ uint32_t lane_now() {
+  uint32_t l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n v_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
+// Segment s of group g from line l0 to the chain's end or l0 + seg_lines.
+// Per-lane addresses are rebuilt from the lane index after each loop, so a
+// relay wave needs no more registers than k_quad_chunks' waves.
+__device__ __forceinline__ void relay_segment(const uint8_t* __restrict__ data, uint64_t bs,
+                                              uint64_t b0, uint32_t nrel, uint32_t g, uint32_t s,
+                                              uint32_t l1_max, uint32_t seg_lines,
+                                              uint32_t* flags, uint64_t* state,
+                                              uint8_t* __restrict__ out, uint8_t* lds,
+                                              bool publish) {
+  const uint32_t lines = (uint32_t)(bs >> 7);
+  const uint32_t l0 = s * seg_lines, l1 = min(l1_max, lines);
+  const bool final = l1 == lines;
+  auto chain = [&](uint32_t lane) { return g * kRelayGroupChains + (lane >> 2); };
+  uint64_t h0, h1;
+  {
+    const uint32_t lane = lane_now();
+    if (s == 0) {
+      quad_init(lane & 3u, h0, h1);
+    } else {
+      const uint64_t* st = state + ((uint64_t)g * 64u + lane) * 2u;
+      h0 = st[0];
+      h1 = st[1];
+    }
+  }
+  uint32_t done = 0;
+  const uint32_t n = l1 - l0;
+  if constexpr (CIR_QUAD_FAST && kQuadAsm) {
+    const uint32_t nu = (final ? n - 1u : n) & ~1u;
+    if (nu >= kQuadFastMin) {
+      const uint32_t lane = lane_now(), c = chain(lane);
+      if (c < nrel) {
+        uint32_t addr[48];
+        quad_addr(addr, (lane >> 2) * 128u, lane & 3u);
+        quad_fast(h0, h1, data + (b0 + c) * bs + (uint64_t)l0 * 128u, nu, lds, addr,
+                  (lane >> 2) * 128u, lane & 3u, l0 * 128u);
+      }
+      done = nu;
+    }
+  }
+  {
+    const uint32_t lane = lane_now(), c = chain(lane);
+    const bool have = c < nrel;
+    uint32_t addr[48];
+    quad_addr(addr, (lane >> 2) * 128u, lane & 3u);
+    quad_run<true>(h0, h1, (uint64_t)(l0 + done) * 128u,
+                   data + (have ? (b0 + c) * bs : 0) + (uint64_t)(l0 + done) * 128u,
+                   have ? (n - done) * 128u : 0u, have, final, lds, addr, (lane >> 2) * 128u,
+                   lane & 3u);
+  }
+  const uint32_t lane = lane_now(), c = chain(lane);
+  if (final) {
+    if (c < nrel) *reinterpret_cast<uint64_t*>(out + (b0 + c) * 32u + 8u * (lane & 3u)) = h0;
+  } else {
+    uint64_t* st = state + ((uint64_t)g * 64u + lane) * 2u;
+    st[0] = h0;
+    st[1] = h1;
+  }
+  if (!publish) return;
+  // the chain values (or digests) reach every XCD's view before the flag
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  if (lane == 0)
+    __hip_atomic_store(flags + g, final ? 0xffffffffu : l1 / seg_lines, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_quad_relay(
+    const uint8_t* __restrict__ data, uint64_t bs, uint64_t b0, uint32_t nrel, uint32_t ngroups,
+    uint32_t seg_lines, uint32_t* flags, uint64_t* state, uint8_t* __restrict__ out,
+    uint32_t max_polls) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kQuadWaveLds];
+  const uint32_t g = blockIdx.x % ngroups, s = blockIdx.x / ngroups;
+  if (s > 0) {
+    // wait at normal priority (s_sleep: the SIMD's lane wave keeps issuing)
+    for (uint32_t r = 0;; ++r) {
+      const uint32_t f = __builtin_amdgcn_readfirstlane(
+          __hip_atomic_load(flags + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      if (f == s) break;
+      if (r >= max_polls) return;  // k_quad_relay_finish takes over from here
+      __builtin_amdgcn_s_sleep(CIR_RELAY_SLEEP);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __builtin_amdgcn_s_setprio(3);
+  relay_segment(data, bs, b0, nrel, g, s, (s + 1u) * seg_lines, seg_lines, flags, state, out, lds,
+                true);
+}
+
+// Behind k_quad_relay on its stream: every group whose last segment has not
+// run (a wave gave up waiting) is finished from its last handed-on state.
+// Then the group's flag goes back to 0 for the next relay on this stream
+// (the scratch's flags are zeroed once, when it is allocated).
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_quad_relay_finish(
+    const uint8_t* __restrict__ data, uint64_t bs, uint64_t b0, uint32_t nrel, uint32_t seg_lines,
+    uint32_t* flags, uint64_t* state, uint8_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kQuadWaveLds];
+  const uint32_t g = blockIdx.x;
+  const uint32_t s = __builtin_amdgcn_readfirstlane(flags[g]);
+  if (s != 0xffffffffu) {  // else the relay finished this group
+    __builtin_amdgcn_s_setprio(3);
+    relay_segment(data, bs, b0, nrel, g, s, 0xffffffffu, seg_lines, flags, state, out, lds,
+                  false);
+  }
+  if (threadIdx.x == 0) flags[g] = 0;
 }
 
 // Quad part of an ordered batch: chains [0, nl), nl = min(*n_long, 64 nq_wg).
@@ -798,7 +965,7 @@ hipError_t launch_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint
   if (bs == 0) return hipErrorInvalidValue;
   const uint64_t nblk = (nbytes + bs - 1) / bs;
   if (chunks_in_quad(nblk, bs)) {
-    hipLaunchKernelGGL(k_quad_chunks, dim3((unsigned)((nblk + 63) / 64)), dim3(kThreads), 0, s,
+    hipLaunchKernelGGL(k_quad_chunks<>, dim3((unsigned)((nblk + 63) / 64)), dim3(kThreads), 0, s,
                        data, nbytes, bs, (uint64_t)0, nblk, out);
     return hipGetLastError();
   }
@@ -821,8 +988,139 @@ hipError_t launch_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint
 // chains and trailed the launch; in quad mode it takes about a third of a
 // lane-mode chain's time.  Forked from s (`fork`), joined back (`join`).
 // Falls back to launch_chunks where the split does not apply.
+// CIR_RELAY=0 turns the relay off (A/B); CIR_RELAY_SEGS = the segment waves
+// one relay aims at (default: one per SIMD).
+#ifndef CIR_RELAY_MAXK
+#define CIR_RELAY_MAXK 16
+#endif
+// With k >= 3 lane waves per SIMD the lane part is launched with
+// kRelayLanePad bytes of extra LDS per workgroup: two k_chunks workgroups
+// per CU (2 x 64 KiB of 160), so two lane waves per SIMD (2 x 112 VGPRs)
+// leave room for a relay wave (272) -- three would not.
+constexpr uint32_t kRelayLanePad = 32768;
+// Quad-regime base (k_quad_chunks: 4 waves, 8 KiB static LDS): padded to
+// 81 KiB per workgroup, one workgroup per CU, so one base wave per SIMD
+// (248 VGPRs) beside a relay wave.
+constexpr uint32_t kRelayQuadPad = 73 * 1024;
+
+static bool relay_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("CIR_RELAY");
+    return !(v && v[0] == '0' && v[1] == 0);
+  }();
+  return on;
+}
+
+static uint64_t relay_target_waves(uint64_t simds) {
+  static const uint64_t v = [] {
+    const char* e = getenv("CIR_RELAY_SEGS");
+    return e ? strtoull(e, nullptr, 10) : 0ull;
+  }();
+  return v ? v : simds;
+}
+
+static uint64_t relay_min_quad_k() {  // CIR_RELAY_QMINK: A/B of the quad-regime floor
+  static const uint64_t v = [] {
+    const char* e = getenv("CIR_RELAY_QMINK");
+    return e ? strtoull(e, nullptr, 10) : 1ull;
+  }();
+  return v;
+}
+
+static uint64_t relay_max_k() {
+  static const uint64_t v = [] {
+    const char* e = getenv("CIR_RELAY_MAXK");
+    return e ? strtoull(e, nullptr, 10) : (uint64_t)CIR_RELAY_MAXK;
+  }();
+  return v;
+}
+
+// How a chunk-form file of nfull whole blocks (+ maybe a short last one)
+// splits when it relays: the first `base` blocks as whole waves on the
+// caller's stream -- lane mode (k_chunks, quad == false) or quad mode
+// (k_quad_chunks, quad == true) -- and blocks [base, base + nrel) relayed
+// on the quad stream.  `pad`: extra LDS per base workgroup that keeps room
+// for a relay wave (240 VGPRs) on every SIMD.
+struct RelayPlan {
+  uint64_t base = 0, nrel = 0;
+  bool quad = false;
+  uint32_t pad = 0;
+};
+
+// Lane regime (nfull >= one lane wave per SIMD): k = 1 .. CIR_RELAY_MAXK whole
+// lane waves per SIMD plus extra blocks up to min(5/8, lines/256) of a lane
+// wave per SIMD; beyond that one more lane wave (or the quad band of
+// chunks_in_quad) costs less than the relayed chains' quad-mode work
+// (profiles/r02/relay/).  Quad regime (below one lane wave per SIMD):
+// k >= 1 whole quad waves per SIMD plus up to 1/4 of one (1/64 past the
+// small-batch limit), chains of >= 128 lines.  16 <= lines, bs < 2^31.
+static bool relay_plan(uint64_t nfull, uint64_t bs, RelayPlan& p) {
+  p = RelayPlan();
+  if (!relay_enabled() || bs % 128u != 0 || bs < 128u * 16u || bs >= (1ull << 31)) return false;
+  const uint64_t simds = device_simds(), lines = bs / 128u;
+  const uint64_t lane_slots = 64ull * simds, quad_slots = 16ull * simds;
+  if (nfull >= lane_slots) {
+    const uint64_t k = nfull / lane_slots, extra = nfull % lane_slots;
+    const uint64_t cap = std::min(lane_slots * 5 / 8, lane_slots * lines / 256);
+    if (k > relay_max_k() || extra == 0 || extra > cap) return false;
+    p.base = nfull - extra;
+    p.nrel = extra;
+    p.pad = k > 2 ? kRelayLanePad : 0u;
+  } else {
+    // chains of >= 128 lines only (at 32 lines the relay's hand-offs cost
+    // more than it saves here); past the small-batch limit (k = 3) lane
+    // mode takes over from 1/64 of a quad wave of extra blocks on
+    const uint64_t k = nfull / quad_slots, extra = nfull % quad_slots;
+    if (lines < 128 || k < relay_min_quad_k() || extra == 0 || extra * 4 > quad_slots ||
+        (nfull >= quad_small_batch() && extra * 64 > quad_slots))
+      return false;
+    p.base = nfull - extra;
+    p.nrel = extra;
+    p.quad = true;
+    p.pad = kRelayQuadPad;
+  }
+  if ((p.nrel + kRelayGroupChains - 1) / kRelayGroupChains > kRelayMaxGroups) return false;
+  return true;
+}
+
+uint64_t relay_blocks(uint64_t nfull, uint64_t bs) {
+  RelayPlan p;
+  return relay_plan(nfull, bs, p) ? p.nrel : 0;
+}
+
+// Blocks [b0, b0 + nrel) of a file of whole bs-byte blocks as relayed quad
+// chains on qs (the relay, then its finisher, which zeroes the flags
+// again).  Segments of at least kRelayMinSegLines lines, as many as make
+// ~one segment wave per SIMD.
+static hipError_t launch_relay(const uint8_t* data, uint64_t bs, uint64_t b0, uint64_t nrel,
+                               uint32_t min_seg, uint8_t* out, hipStream_t qs,
+                               const RelayScratch& r) {
+  const uint32_t lines = (uint32_t)(bs / 128u);
+  const uint32_t groups = (uint32_t)((nrel + kRelayGroupChains - 1) / kRelayGroupChains);
+  if (groups > r.groups) return hipErrorInvalidValue;
+  const uint64_t target = relay_target_waves(device_simds());
+  uint32_t nseg = (uint32_t)std::max<uint64_t>(1, target / groups);
+  nseg = std::min(nseg, std::max(1u, lines / min_seg));
+  uint32_t seg = ((lines + nseg - 1) / nseg + 1u) & ~1u;
+  nseg = (lines + seg - 1) / seg;
+  // each poll takes >= ~0.5 us (the sleep and an L2-missing load); a segment
+  // waits at most for the chain before it (~1.1-2.5 us per line), so this
+  // bound is never reached in a healthy run (CIR_RELAY_POLLS overrides it,
+  // read per call: the finisher test)
+  uint32_t max_polls = std::max<uint32_t>(32768u, lines * 64u);
+  if (const char* v = getenv("CIR_RELAY_POLLS")) max_polls = (uint32_t)strtoul(v, nullptr, 10);
+  hipLaunchKernelGGL(k_quad_relay, dim3(groups * nseg), dim3(64), 0, qs, data, bs, b0,
+                     (uint32_t)nrel, groups, seg, r.flags, r.state, out, max_polls);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_quad_relay_finish, dim3(groups), dim3(64), 0, qs, data, bs, b0,
+                     (uint32_t)nrel, seg, r.flags, r.state, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_chunks_split(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint8_t* out,
-                               hipStream_t s, hipStream_t qs, hipEvent_t fork, hipEvent_t join) {
+                               hipStream_t s, hipStream_t qs, hipEvent_t fork, hipEvent_t join,
+                               const RelayScratch* relay) {
   if (nbytes == 0) return hipSuccess;
   if (bs == 0) return hipErrorInvalidValue;
   const uint64_t nblk = (nbytes + bs - 1) / bs;
@@ -830,13 +1128,44 @@ hipError_t launch_chunks_split(const uint8_t* data, uint64_t nbytes, uint64_t bs
   const bool uni_ok = bs % 128u == 0 && (reinterpret_cast<uintptr_t>(data) & 15u) == 0 &&
                       bs / 128u <= 0xffffffffull && bs <= 0xffffffffull / 8u;
   const uint64_t grid = grid_for(grid_for(nfull, 64), kWaves);
+  RelayPlan plan;
+  if (relay && relay->flags && qs && qs != s && uni_ok && relay_plan(nfull, bs, plan)) {
+    // k whole lane (or quad) waves per SIMD on s, enqueued first so they
+    // start at once (the relay fits beside them); the extra whole blocks
+    // relayed and the short last block (if any) in quad mode, both on qs
+    hipError_t e = hipEventRecord(fork, s);
+    if (e != hipSuccess) return e;
+    if (plan.quad)
+      hipLaunchKernelGGL(k_quad_chunks<true>, dim3((unsigned)grid_for(plan.base, 64)),
+                         dim3(kThreads), plan.pad, s, data, nbytes, bs, (uint64_t)0, plan.base,
+                         out);
+    else
+      hipLaunchKernelGGL(k_chunks, dim3((unsigned)grid_for(grid_for(plan.base, 64), kWaves)),
+                         dim3(kThreads), plan.pad, s, data, nbytes, bs, (uint32_t)(bs / 128u),
+                         plan.base, 0u, out);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamWaitEvent(qs, fork, 0);
+    if (e != hipSuccess) return e;
+    if (nfull < nblk) {
+      hipLaunchKernelGGL(k_quad_chunks<>, dim3(1), dim3(kThreads), 0, qs, data, nbytes, bs, nfull,
+                         nblk, out);
+      e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    e = launch_relay(data, bs, plan.base, plan.nrel, plan.quad ? 16u : kRelayMinSegLines, out, qs,
+                     *relay);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipEventRecord(join, qs);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
+    return e;
+  }
   if (!qs || qs == s || chunks_in_quad(nblk, bs) || !uni_ok || nfull == nblk ||
       bs < 128ull * kQuadSmallMinLines || grid > 0x7fffffffull)
     return launch_chunks(data, nbytes, bs, out, s);
   hipError_t e = hipEventRecord(fork, s);
   if (e == hipSuccess) e = hipStreamWaitEvent(qs, fork, 0);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_quad_chunks, dim3(1), dim3(kThreads), 0, qs, data, nbytes, bs, nfull, nblk,
+  hipLaunchKernelGGL(k_quad_chunks<>, dim3(1), dim3(kThreads), 0, qs, data, nbytes, bs, nfull, nblk,
                      out);
   e = hipGetLastError();
   if (e != hipSuccess) return e;

@@ -55,11 +55,28 @@ hipError_t launch_uniform(Loader loader, const uint8_t* data, uint64_t bs, uint6
 hipError_t launch_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint8_t* out,
                          hipStream_t s);
 
+// Device scratch of the relay (k_quad_relay): a flag and 64 x 16 B of chain
+// values per group of 16 chains (one quad-mode wave).  Used on qs only,
+// so calls on one device's qs need no other ordering.
+struct RelayScratch {
+  uint32_t* flags = nullptr;
+  uint64_t* state = nullptr;
+  uint32_t groups = 0;  // capacity
+};
+constexpr uint32_t kRelayMaxGroups = 4096;
+inline size_t relay_scratch_bytes(uint32_t groups) { return (size_t)groups * (4 + 64 * 16); }
+
 // launch_chunks with the ragged rest in quad mode on qs, concurrently with
-// the uniform part on s (fork / join events); launch_chunks where that does
-// not apply (small or misaligned files, no rest, qs null or == s).
+// the uniform part on s (fork / join events); a file of k whole lane waves
+// per SIMD plus a few blocks (k = 1, 2) runs the extra blocks as relayed
+// quad chains on qs (relay, when given); launch_chunks where neither
+// applies (small or misaligned files, no rest, qs null or == s).
 hipError_t launch_chunks_split(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint8_t* out,
-                               hipStream_t s, hipStream_t qs, hipEvent_t fork, hipEvent_t join);
+                               hipStream_t s, hipStream_t qs, hipEvent_t fork, hipEvent_t join,
+                               const RelayScratch* relay = nullptr);
+// Number of blocks launch_chunks_split would relay (0: no relay) for a file
+// of nfull whole blocks of bs bytes on the current device.
+uint64_t relay_blocks(uint64_t nfull, uint64_t bs);
 
 // Blocks first .. first+n-1 of Hashes::hash_file's split of [data, data+nbytes).
 hipError_t launch_general_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs,

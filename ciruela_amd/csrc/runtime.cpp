@@ -59,6 +59,7 @@ Device::~Device() {
   if (order_free) (void)hipEventDestroy(order_free);
   if (aux) (void)hipStreamSynchronize(aux);
   if (qstream) (void)hipStreamSynchronize(qstream);
+  (void)hipFree(relay_mem);
   if (aux_fork) (void)hipEventDestroy(aux_fork);
   if (aux_join) (void)hipEventDestroy(aux_join);
   if (q_join) (void)hipEventDestroy(q_join);
@@ -664,8 +665,19 @@ int cir_hash_chunks_dev(cir_ctx* ctx, const void* d_data, uint64_t nbytes, uint6
     CIR_HIP(hipSetDevice(d->id));
     int rc = ensure_part_streams(*d);
     if (rc) return rc;
+    const uint64_t nfull = nbytes / block_size;
+    if (!d->relay_mem && dev::relay_blocks(nfull, block_size) > 0) {
+      // first relayed file on this device: chain values, then the flags
+      const size_t bytes = dev::relay_scratch_bytes(dev::kRelayMaxGroups);
+      CIR_HIP(hipMalloc(&d->relay_mem, bytes));
+      d->relay.state = (uint64_t*)d->relay_mem;
+      d->relay.flags = (uint32_t*)((uint8_t*)d->relay_mem + (size_t)dev::kRelayMaxGroups * 1024u);
+      d->relay.groups = dev::kRelayMaxGroups;
+      // zeroed once; each relay's finisher zeroes its groups' flags again
+      CIR_HIP(hipMemsetAsync(d->relay.flags, 0, (size_t)dev::kRelayMaxGroups * 4u, d->qstream));
+    }
     CIR_HIP(dev::launch_chunks_split((const uint8_t*)d_data, nbytes, block_size, d_out, s,
-                                     d->qstream, d->aux_fork, d->q_join));
+                                     d->qstream, d->aux_fork, d->q_join, &d->relay));
     return CIR_OK;
   }
   CIR_HIP(dev::launch_chunks((const uint8_t*)d_data, nbytes, block_size, d_out, s));
@@ -992,6 +1004,10 @@ int cir_debug_compress_only_dev(uint64_t nlanes, uint32_t lines, uint8_t* d_out,
     return fail(CIR_EINVAL, "compress-only kernel needs nlanes % 256 == 0, lines > 0, an output");
   CIR_HIP(dev::launch_compress_only(nlanes, lines, d_out, (hipStream_t)stream));
   return CIR_OK;
+}
+
+uint64_t cir_debug_relay_blocks(uint64_t nfull, uint64_t block_size) {
+  return dev::relay_blocks(nfull, block_size);
 }
 
 int cir_fill_splitmix64_dev(void* d_ptr, uint64_t nbytes, uint64_t seed, uint64_t block_bytes,

@@ -91,6 +91,10 @@ struct Device {
   int part_mode = 0;
   hipStream_t aux = nullptr, qstream = nullptr;
   hipEvent_t aux_fork = nullptr, aux_join = nullptr, q_join = nullptr;
+  // relayed quad chains of cir_hash_chunks_dev (used on qstream only;
+  // allocated at full capacity on first use, under order_mu)
+  dev::RelayScratch relay;
+  void* relay_mem = nullptr;
   // incremental footer chain (cir_scan_v1): own stream, state, text buffers
   std::mutex chain_mu;  // one incremental footer (scan) at a time per device
   hipStream_t chain = nullptr;

@@ -226,6 +226,12 @@ int cir_debug_hash_uniform_dev(int loader, const void* d_data, uint64_t block_si
  * memory traffic.  bench.py times it as the measured VALU ceiling. */
 int cir_debug_compress_only_dev(uint64_t nlanes, uint32_t lines, uint8_t* d_out, void* stream);
 
+/* How many whole blocks of a file of nfull x block_size bytes (plus any short
+ * last block) cir_hash_chunks_dev with a context relays on the calling
+ * thread's current device (0: none).  Relayed blocks run in quad mode as
+ * segmented chains beside k = 1 or 2 whole lane waves per SIMD. */
+uint64_t cir_debug_relay_blocks(uint64_t nfull, uint64_t block_size);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1020,3 +1020,85 @@ def test_chunks_dev_without_context(gpu, oracle, bs, nbytes):
     torch.cuda.synchronize()
     want = oracle_chunks(oracle, data.cpu().numpy(), nbytes, bs)
     assert first_bad(out.cpu().numpy(), want) is None
+
+
+def lane_wave_slots():
+    import torch
+    return 64 * 4 * torch.cuda.get_device_properties(0).multi_processor_count
+
+
+# (block size, whole waves per SIMD k -- lane waves of 64 chains, or quad
+# waves of 16 ("q") below the small-batch limit -- extra whole blocks, tail)
+RELAY_SHAPES = [
+    (32768, 1, 1, 0),          # one extra chain: 16 segments of 16 lines
+    (32768, 1, 1000, 777),     # 63 groups + the short last block beside
+    (4096, 2, 5000, 1),        # k = 2, 32-line chains: 2 segments each
+    (2048, 1, 4000, 0),        # 250 groups of 16-line chains: one segment each
+    (131072, 1, 3, 0),         # 1024-line chains: 64 segments
+    (4096, 4, 100, 5),         # k >= 3: the lane part with padded LDS (2 waves per SIMD)
+    (32768, "2q", 1, 0),       # quad regime: 2 quad waves per SIMD + 1 chain
+    (16384, "2q", 3000, 99),   # 2 quad waves per SIMD + 3000 chains + a tail
+    (65536, "1q", 2, 0),       # 1 quad wave per SIMD + 2 chains
+    (32768, "3q", 4, 0),       # past the small-batch limit: quad base of 3 waves
+]
+
+
+def relay_nfull(k, extra):
+    slots = lane_wave_slots()
+    if isinstance(k, str):
+        return int(k[:-1]) * slots // 4 + extra
+    return k * slots + extra
+
+
+@pytest.mark.parametrize("bs,k,extra,tail", RELAY_SHAPES)
+@pytest.mark.parametrize("polls", [None, "0"])
+def test_chunks_dev_relay(gpu, ctx, oracle, bs, k, extra, tail, polls, monkeypatch):
+    """A file of k whole lane waves per SIMD plus `extra` blocks: the extra
+    blocks run as relayed quad chains (k_quad_relay) beside the lane part.
+    polls "0": every waiting segment gives up at once, so the finisher
+    (k_quad_relay_finish) completes the chains from the handed-on state."""
+    import torch
+    if polls is not None:
+        monkeypatch.setenv("CIR_RELAY_POLLS", polls)
+    nfull = relay_nfull(k, extra)
+    assert gpu._n.lib.cir_debug_relay_blocks(nfull, bs) == extra
+    nbytes = nfull * bs + tail
+    data = dev_random(gpu, nbytes, seed=nfull ^ bs)
+    nb = (nbytes + bs - 1) // bs
+    out = torch.zeros(nb * 32, dtype=torch.uint8, device="cuda:0")
+    for _ in range(2):  # the second call reuses the flags and the state buffer
+        ctx.hash_chunks_dev(data.data_ptr(), nbytes, bs, out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    want = oracle_chunks(oracle, data.cpu().numpy(), nbytes, bs)
+    del data
+    assert first_bad(out.cpu().numpy(), want) is None, "block %s" % first_bad(out.cpu().numpy(), want)
+
+
+def test_relay_rule_bounds(gpu):
+    """No relay below one quad wave per SIMD, beyond k = 16 lane waves, past
+    5/8 of a lane wave (lines / 256 for short chains) or 1/4 of a quad wave
+    (1/64 past the small-batch limit) of extra blocks, below 16 lines, or in
+    the quad regime below 128 lines."""
+    slots = lane_wave_slots()
+    qslots = slots // 4
+    f = gpu._n.lib.cir_debug_relay_blocks
+    assert f(slots - 1, 32768) == 0
+    assert f(slots, 32768) == 0
+    assert f(slots + 1, 32768) == 1
+    assert f(3 * slots + 1, 32768) == 1
+    assert f(16 * slots + 5, 32768) == 5
+    assert f(17 * slots + 1, 32768) == 0
+    assert f(slots + slots * 5 // 8, 32768) == slots * 5 // 8
+    assert f(slots + slots * 5 // 8 + 1, 32768) == 0
+    assert f(slots + slots // 8, 4096) == slots // 8
+    assert f(slots + slots // 8 + 1, 4096) == 0
+    assert f(slots + 1, 1024) == 0
+    assert f(slots + 1, 2048) == 1
+    assert f(qslots - 1, 32768) == 0
+    assert f(qslots + 1, 32768) == 1
+    assert f(qslots + 1, 8192) == 0
+    assert f(2 * qslots + 1, 32768) == 1
+    assert f(2 * qslots + qslots // 4, 32768) == qslots // 4
+    assert f(2 * qslots + qslots // 4 + 1, 32768) == 0
+    assert f(3 * qslots + qslots // 64, 32768) == qslots // 64
+    assert f(3 * qslots + qslots // 64 + 1, 32768) == 0
