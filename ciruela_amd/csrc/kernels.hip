@@ -439,9 +439,7 @@ constexpr uint32_t kRelayGroupChains = 16;
 // Each segment adds its lines' quad-mode work (~1 us per line) to the lane
 // wave of the SIMD it lands on, so short chains take short segments: at
 // 32 lines, 16-line segments cost the lane part 12 %.  8 = the hand-
-// scheduled loop's minimum (kQuadFastMin).  Beside quad-mode base waves the
-// relayed chain is as long as the base's and every hand-off (~2-4 us) adds
-// to it, so segments there are 16 lines or more.
+// scheduled loop's minimum (kQuadFastMin).  Each hand-off costs ~4 us.
 constexpr uint32_t kRelayMinSegLines = 8;
 
 // Lines [l0, l1) of a chain of full 128-B lines at blk (16-B aligned);
@@ -1045,6 +1043,8 @@ struct RelayPlan {
   uint64_t base = 0, nrel = 0;
   bool quad = false;
   uint32_t pad = 0;
+  uint32_t min_seg = kRelayMinSegLines;  // shortest segment (lines)
+  bool relay_first = false;              // enqueue the relay before the base
 };
 
 // Lane regime (nfull >= one lane wave per SIMD): k = 1 .. CIR_RELAY_MAXK whole
@@ -1078,6 +1078,11 @@ static bool relay_plan(uint64_t nfull, uint64_t bs, RelayPlan& p) {
     p.nrel = extra;
     p.quad = true;
     p.pad = kRelayQuadPad;
+    // beside quad-mode base waves the relayed chain has less slack (none at
+    // k = 1: it is as long as the base's, and every hand-off adds to it), so
+    // longer segments: 16 lines, 32 at k = 1, where it also starts first
+    p.min_seg = k == 1 ? 32u : 16u;
+    p.relay_first = k == 1;
   }
   if ((p.nrel + kRelayGroupChains - 1) / kRelayGroupChains > kRelayMaxGroups) return false;
   return true;
@@ -1130,31 +1135,35 @@ hipError_t launch_chunks_split(const uint8_t* data, uint64_t nbytes, uint64_t bs
   const uint64_t grid = grid_for(grid_for(nfull, 64), kWaves);
   RelayPlan plan;
   if (relay && relay->flags && qs && qs != s && uni_ok && relay_plan(nfull, bs, plan)) {
-    // k whole lane (or quad) waves per SIMD on s, enqueued first so they
-    // start at once (the relay fits beside them); the extra whole blocks
-    // relayed and the short last block (if any) in quad mode, both on qs
+    // k whole lane (or quad) waves per SIMD on s; the extra whole blocks
+    // relayed and the short last block (if any) in quad mode, both on qs.
+    // The longer part is enqueued first, so it starts first: the base, or
+    // the relay when its chain is as long as the base's (quad regime, k = 1).
     hipError_t e = hipEventRecord(fork, s);
-    if (e != hipSuccess) return e;
-    if (plan.quad)
-      hipLaunchKernelGGL(k_quad_chunks<true>, dim3((unsigned)grid_for(plan.base, 64)),
-                         dim3(kThreads), plan.pad, s, data, nbytes, bs, (uint64_t)0, plan.base,
-                         out);
-    else
-      hipLaunchKernelGGL(k_chunks, dim3((unsigned)grid_for(grid_for(plan.base, 64), kWaves)),
-                         dim3(kThreads), plan.pad, s, data, nbytes, bs, (uint32_t)(bs / 128u),
-                         plan.base, 0u, out);
-    e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamWaitEvent(qs, fork, 0);
     if (e != hipSuccess) return e;
-    if (nfull < nblk) {
-      hipLaunchKernelGGL(k_quad_chunks<>, dim3(1), dim3(kThreads), 0, qs, data, nbytes, bs, nfull,
-                         nblk, out);
-      e = hipGetLastError();
-      if (e != hipSuccess) return e;
-    }
-    e = launch_relay(data, bs, plan.base, plan.nrel, plan.quad ? 16u : kRelayMinSegLines, out, qs,
-                     *relay);
-    e = hipGetLastError();
+    auto base = [&]() -> hipError_t {
+      if (plan.quad)
+        hipLaunchKernelGGL(k_quad_chunks<true>, dim3((unsigned)grid_for(plan.base, 64)),
+                           dim3(kThreads), plan.pad, s, data, nbytes, bs, (uint64_t)0, plan.base,
+                           out);
+      else
+        hipLaunchKernelGGL(k_chunks, dim3((unsigned)grid_for(grid_for(plan.base, 64), kWaves)),
+                           dim3(kThreads), plan.pad, s, data, nbytes, bs, (uint32_t)(bs / 128u),
+                           plan.base, 0u, out);
+      return hipGetLastError();
+    };
+    auto rest = [&]() -> hipError_t {
+      if (nfull < nblk) {
+        hipLaunchKernelGGL(k_quad_chunks<>, dim3(1), dim3(kThreads), 0, qs, data, nbytes, bs,
+                           nfull, nblk, out);
+        const hipError_t e2 = hipGetLastError();
+        if (e2 != hipSuccess) return e2;
+      }
+      return launch_relay(data, bs, plan.base, plan.nrel, plan.min_seg, out, qs, *relay);
+    };
+    e = plan.relay_first ? rest() : base();
+    if (e == hipSuccess) e = plan.relay_first ? base() : rest();
     if (e == hipSuccess) e = hipEventRecord(join, qs);
     if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
     return e;
