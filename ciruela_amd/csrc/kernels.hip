@@ -10,6 +10,10 @@
 //                      into VGPRs one line ahead (A/B variant of the loader).
 //   k_quad_chunks    : small files (< kQuadSmallBatch blocks): 4 lanes per
 //                      block chain, 16 chains per wave (DPP quad_perm).
+//   k_quad_relay +
+//   k_quad_relay_fin.: the blocks of a file past k whole waves per SIMD, as
+//                      quad chains cut into segments handed from wave to
+//                      wave (beside the k waves of k_chunks / k_quad_chunks).
 //   k_quad_long +
 //   k_lane_rest      : descriptor batches ordered longest chain first: long
 //                      chains in quad mode, the rest one lane per chain.
