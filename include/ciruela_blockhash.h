@@ -80,7 +80,11 @@ int cir_blake2b256(const uint8_t* p, size_t n, uint8_t out[CIR_DIGEST_BYTES]);
  * one file already in HBM, split into ceil(nbytes / block_size) blocks (the
  * last one short; none when nbytes == 0), digest i -> d_out + 32 i (d_out
  * 16-byte aligned, as hipMalloc returns it).  This is the metric path
- * (BASELINE.json configs 2 and 4). */
+ * (BASELINE.json configs 2 and 4).  With a context (ctx != NULL) parts of
+ * the file may also run on the device's own quad-part stream (the short last
+ * block; the blocks past a whole number of waves per SIMD), forked from and
+ * joined back into `stream`, so the call is ordered on `stream` as one
+ * launch would be; ctx == NULL: one launch on `stream`, no side streams. */
 int cir_hash_chunks_dev(cir_ctx* ctx, const void* d_data, uint64_t nbytes, uint64_t block_size,
                         uint8_t* d_out, void* stream);
 
@@ -229,7 +233,7 @@ int cir_debug_compress_only_dev(uint64_t nlanes, uint32_t lines, uint8_t* d_out,
 /* How many whole blocks of a file of nfull x block_size bytes (plus any short
  * last block) cir_hash_chunks_dev with a context relays on the calling
  * thread's current device (0: none).  Relayed blocks run in quad mode as
- * segmented chains beside k = 1 or 2 whole lane waves per SIMD. */
+ * segmented chains beside k whole lane (or quad) waves per SIMD. */
 uint64_t cir_debug_relay_blocks(uint64_t nfull, uint64_t block_size);
 
 #ifdef __cplusplus
