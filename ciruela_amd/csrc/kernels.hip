@@ -279,40 +279,65 @@ __device__ __forceinline__ void quad_run(uint64_t& h0, uint64_t& h1, uint64_t t0
 // part is read; the repeats are never used); compression j reads line j+1's
 // message words while it runs.  No branch, no compiler-inserted wait
 // between compressions.
-__device__ __forceinline__ void quad_fast(uint64_t& h0, uint64_t& h1, const uint8_t* p,
-                                          uint32_t nu, uint8_t* lds,
-                                          const uint32_t (&addr)[48], uint32_t line,
-                                          uint32_t i, uint32_t t0 = 0) {
-  const uint64_t cv = iv_lo(i), dv0 = iv_hi(i);
-  const uint32_t m0 = i == 0 ? ~0u : 0u;  // lane 0 of the quad carries t
+// quad_fast in two halves: quad_fast_begin loads the first three lines and
+// reads line 0's message words (no chain value needed yet), quad_fast_run
+// compresses.  The relay (k_quad_relay) runs the first half while its
+// segment waits for the predecessor's chain value.
+struct QuadFast {
+  uint64_t ma[40], mb[40];
+  uint32_t pa[40];
+  uint32_t wr;
+  u32x4 u0, w0, u1, w1;
+  const uint8_t* ptr;
+};
+
+__device__ __forceinline__ void quad_fast_begin(QuadFast& f, const uint8_t* p, uint8_t* lds,
+                                                const uint32_t (&addr)[48], uint32_t line,
+                                                uint32_t i) {
   // LDS byte address of the kernel's shared array: a generic pointer into
   // LDS is the shared aperture's base in its high half and the LDS offset in
   // its low half, so the low 32 bits are what ds_read / ds_write take
   const uint32_t base = (uint32_t)reinterpret_cast<uintptr_t>(lds);
-  uint32_t pa[40];
 #pragma unroll
-  for (int k = 0; k < 40; ++k) pa[k] = base + addr[k];
-  const uint32_t wr = base + line + 32u * i;
+  for (int k = 0; k < 40; ++k) f.pa[k] = base + addr[k];
+  f.wr = base + line + 32u * i;
   const uint8_t* src = p + 32u * i;
-  uint64_t ma[40], mb[40];
   const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
   *reinterpret_cast<u32x4*>(lds + line + 32u * i) = s4[0];
   *reinterpret_cast<u32x4*>(lds + line + 32u * i + 16u) = s4[1];
-  quad_read_msg(ma, lds, addr);
-  u32x4 u1 = s4[8], w1 = s4[9], u0 = s4[16], w0 = s4[17];  // lines 1 and 2
+  quad_read_msg(f.ma, lds, addr);
+  f.u1 = s4[8];  // lines 1 and 2
+  f.w1 = s4[9];
+  f.u0 = s4[16];
+  f.w0 = s4[17];
   // the compiler's own waits for these loads go here, not into the loop
-  asm volatile("" : "+v"(u1), "+v"(w1), "+v"(u0), "+v"(w0));
-  const uint8_t* ptr = src + 384;
+  asm volatile("" : "+v"(f.u1), "+v"(f.w1), "+v"(f.u0), "+v"(f.w0));
+  f.ptr = src + 384;
+}
+
+__device__ __forceinline__ void quad_fast_run(QuadFast& f, uint64_t& h0, uint64_t& h1,
+                                              uint32_t nu, uint32_t i, uint32_t t0) {
+  const uint64_t cv = iv_lo(i), dv0 = iv_hi(i);
+  const uint32_t m0 = i == 0 ? ~0u : 0u;  // lane 0 of the quad carries t
   const uint32_t dl = lo32(dv0), dh = hi32(dv0);
   for (uint32_t j = 0; j < nu; j += 2) {
-    compress_quad_fast(h0, h1, cv, dl, dh, t0 + (j + 1u) * 128u, m0, ma, mb, pa, wr, u1, w1,
-                       ptr, j + 4u < nu ? 128u : 0u);
-    compress_quad_fast(h0, h1, cv, dl, dh, t0 + (j + 2u) * 128u, m0, mb, ma, pa, wr, u0, w0,
-                       ptr, j + 5u < nu ? 128u : 0u);
+    compress_quad_fast(h0, h1, cv, dl, dh, t0 + (j + 1u) * 128u, m0, f.ma, f.mb, f.pa, f.wr, f.u1,
+                       f.w1, f.ptr, j + 4u < nu ? 128u : 0u);
+    compress_quad_fast(h0, h1, cv, dl, dh, t0 + (j + 2u) * 128u, m0, f.mb, f.ma, f.pa, f.wr, f.u0,
+                       f.w0, f.ptr, j + 5u < nu ? 128u : 0u);
   }
   // the last loads are in flight into u0/w0/u1/w1: keep the registers until
   // they have landed
-  asm volatile("s_waitcnt vmcnt(0)" ::"v"(u0), "v"(w0), "v"(u1), "v"(w1) : "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::"v"(f.u0), "v"(f.w0), "v"(f.u1), "v"(f.w1) : "memory");
+}
+
+__device__ __forceinline__ void quad_fast(uint64_t& h0, uint64_t& h1, const uint8_t* p,
+                                          uint32_t nu, uint8_t* lds,
+                                          const uint32_t (&addr)[48], uint32_t line,
+                                          uint32_t i, uint32_t t0 = 0) {
+  QuadFast f;
+  quad_fast_begin(f, p, lds, addr, line, i);
+  quad_fast_run(f, h0, h1, nu, i, t0);
 }
 
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
@@ -477,17 +502,49 @@ __device__ __forceinline__ uint32_t lane_now() {
 
 // Segment s of group g from line l0 to the chain's end or l0 + seg_lines.
 // Per-lane addresses are rebuilt from the lane index after each loop, so a
-// relay wave needs no more registers than k_quad_chunks' waves.
+// relay wave needs no more registers than k_quad_chunks' waves.  max_polls
+// > 0: wait for the predecessor's flag first (0 = the finisher, which does
+// not wait); the segment's first lines are loaded before the wait, so a
+// hand-off costs the flag and the chain value's round trips only.  Returns
+// early (nothing written) when the wait gives up.
 __device__ __forceinline__ void relay_segment(const uint8_t* __restrict__ data, uint64_t bs,
                                               uint64_t b0, uint32_t nrel, uint32_t g, uint32_t s,
                                               uint32_t l1_max, uint32_t seg_lines,
                                               uint32_t* flags, uint64_t* state,
                                               uint8_t* __restrict__ out, uint8_t* lds,
-                                              bool publish) {
+                                              uint32_t max_polls, bool publish) {
   const uint32_t lines = (uint32_t)(bs >> 7);
   const uint32_t l0 = s * seg_lines, l1 = min(l1_max, lines);
   const bool final = l1 == lines;
   auto chain = [&](uint32_t lane) { return g * kRelayGroupChains + (lane >> 2); };
+  const uint32_t n = l1 - l0;
+  uint32_t nu = 0;
+  if constexpr (CIR_QUAD_FAST && kQuadAsm) {
+    nu = (final ? n - 1u : n) & ~1u;
+    if (nu < kQuadFastMin) nu = 0;
+  }
+  QuadFast f;
+  if (nu) {
+    const uint32_t lane = lane_now(), c = chain(lane);
+    if (c < nrel) {
+      uint32_t addr[48];
+      quad_addr(addr, (lane >> 2) * 128u, lane & 3u);
+      quad_fast_begin(f, data + (b0 + c) * bs + (uint64_t)l0 * 128u, lds, addr,
+                      (lane >> 2) * 128u, lane & 3u);
+    }
+  }
+  if (s > 0 && max_polls) {
+    // wait at normal priority (s_sleep: the SIMD's other waves keep issuing)
+    for (uint32_t r = 0;; ++r) {
+      const uint32_t fl = __builtin_amdgcn_readfirstlane(
+          __hip_atomic_load(flags + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      if (fl == s) break;
+      if (r >= max_polls) return;  // k_quad_relay_finish takes over from here
+      __builtin_amdgcn_s_sleep(CIR_RELAY_SLEEP);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __builtin_amdgcn_s_setprio(3);
   uint64_t h0, h1;
   {
     const uint32_t lane = lane_now();
@@ -499,29 +556,18 @@ __device__ __forceinline__ void relay_segment(const uint8_t* __restrict__ data, 
       h1 = st[1];
     }
   }
-  uint32_t done = 0;
-  const uint32_t n = l1 - l0;
-  if constexpr (CIR_QUAD_FAST && kQuadAsm) {
-    const uint32_t nu = (final ? n - 1u : n) & ~1u;
-    if (nu >= kQuadFastMin) {
-      const uint32_t lane = lane_now(), c = chain(lane);
-      if (c < nrel) {
-        uint32_t addr[48];
-        quad_addr(addr, (lane >> 2) * 128u, lane & 3u);
-        quad_fast(h0, h1, data + (b0 + c) * bs + (uint64_t)l0 * 128u, nu, lds, addr,
-                  (lane >> 2) * 128u, lane & 3u, l0 * 128u);
-      }
-      done = nu;
-    }
+  if (nu) {
+    const uint32_t lane = lane_now();
+    if (chain(lane) < nrel) quad_fast_run(f, h0, h1, nu, lane & 3u, l0 * 128u);
   }
   {
     const uint32_t lane = lane_now(), c = chain(lane);
     const bool have = c < nrel;
     uint32_t addr[48];
     quad_addr(addr, (lane >> 2) * 128u, lane & 3u);
-    quad_run<true>(h0, h1, (uint64_t)(l0 + done) * 128u,
-                   data + (have ? (b0 + c) * bs : 0) + (uint64_t)(l0 + done) * 128u,
-                   have ? (n - done) * 128u : 0u, have, final, lds, addr, (lane >> 2) * 128u,
+    quad_run<true>(h0, h1, (uint64_t)(l0 + nu) * 128u,
+                   data + (have ? (b0 + c) * bs : 0) + (uint64_t)(l0 + nu) * 128u,
+                   have ? (n - nu) * 128u : 0u, have, final, lds, addr, (lane >> 2) * 128u,
                    lane & 3u);
   }
   const uint32_t lane = lane_now(), c = chain(lane);
@@ -546,20 +592,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     uint32_t max_polls) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kQuadWaveLds];
   const uint32_t g = blockIdx.x % ngroups, s = blockIdx.x / ngroups;
-  if (s > 0) {
-    // wait at normal priority (s_sleep: the SIMD's lane wave keeps issuing)
-    for (uint32_t r = 0;; ++r) {
-      const uint32_t f = __builtin_amdgcn_readfirstlane(
-          __hip_atomic_load(flags + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      if (f == s) break;
-      if (r >= max_polls) return;  // k_quad_relay_finish takes over from here
-      __builtin_amdgcn_s_sleep(CIR_RELAY_SLEEP);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
-  __builtin_amdgcn_s_setprio(3);
   relay_segment(data, bs, b0, nrel, g, s, (s + 1u) * seg_lines, seg_lines, flags, state, out, lds,
-                true);
+                max_polls ? max_polls : 1u, true);
 }
 
 // Behind k_quad_relay on its stream: every group whose last segment has not
@@ -572,11 +606,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   __shared__ __attribute__((aligned(16))) uint8_t lds[kQuadWaveLds];
   const uint32_t g = blockIdx.x;
   const uint32_t s = __builtin_amdgcn_readfirstlane(flags[g]);
-  if (s != 0xffffffffu) {  // else the relay finished this group
-    __builtin_amdgcn_s_setprio(3);
-    relay_segment(data, bs, b0, nrel, g, s, 0xffffffffu, seg_lines, flags, state, out, lds,
+  if (s != 0xffffffffu)  // else the relay finished this group
+    relay_segment(data, bs, b0, nrel, g, s, 0xffffffffu, seg_lines, flags, state, out, lds, 0u,
                   false);
-  }
   if (threadIdx.x == 0) flags[g] = 0;
 }
 
@@ -1029,6 +1061,14 @@ static uint64_t relay_min_quad_k() {  // CIR_RELAY_QMINK: A/B of the quad-regime
   return v;
 }
 
+static uint32_t relay_quad1_seg() {  // CIR_RELAY_QSEG1: A/B of the k = 1 quad segments
+  static const uint32_t v = [] {
+    const char* e = getenv("CIR_RELAY_QSEG1");
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : 32u;
+  }();
+  return std::max<uint32_t>(v, kRelayMinSegLines);
+}
+
 static uint64_t relay_max_k() {
   static const uint64_t v = [] {
     const char* e = getenv("CIR_RELAY_MAXK");
@@ -1085,7 +1125,7 @@ static bool relay_plan(uint64_t nfull, uint64_t bs, RelayPlan& p) {
     // beside quad-mode base waves the relayed chain has less slack (none at
     // k = 1: it is as long as the base's, and every hand-off adds to it), so
     // longer segments: 16 lines, 32 at k = 1, where it also starts first
-    p.min_seg = k == 1 ? 32u : 16u;
+    p.min_seg = k == 1 ? relay_quad1_seg() : 16u;
     p.relay_first = k == 1;
   }
   if ((p.nrel + kRelayGroupChains - 1) / kRelayGroupChains > kRelayMaxGroups) return false;
