@@ -1061,6 +1061,12 @@ static uint64_t relay_min_quad_k() {  // CIR_RELAY_QMINK: A/B of the quad-regime
   return v;
 }
 
+// tuning probes (read per call; diagnostics of the quad-regime rule)
+static uint64_t relay_env(const char* name, uint64_t dflt) {
+  const char* e = getenv(name);
+  return e ? strtoull(e, nullptr, 10) : dflt;
+}
+
 static uint32_t relay_quad1_seg() {  // CIR_RELAY_QSEG1: A/B of the k = 1 quad segments
   static const uint32_t v = [] {
     const char* e = getenv("CIR_RELAY_QSEG1");
@@ -1097,7 +1103,8 @@ struct RelayPlan {
 // chunks_in_quad) costs less than the relayed chains' quad-mode work
 // (profiles/r02/relay/).  Quad regime (below one lane wave per SIMD):
 // k >= 1 whole quad waves per SIMD plus up to 1/4 of one (1/64 past the
-// small-batch limit), chains of >= 128 lines.  16 <= lines, bs < 2^31.
+// small-batch limit), chains of >= 64 lines at k = 1 (>= 32 above: shorter
+// relays cost more than they save).  16 <= lines, bs < 2^31.
 static bool relay_plan(uint64_t nfull, uint64_t bs, RelayPlan& p) {
   p = RelayPlan();
   if (!relay_enabled() || bs % 128u != 0 || bs < 128u * 16u || bs >= (1ull << 31)) return false;
@@ -1115,18 +1122,21 @@ static bool relay_plan(uint64_t nfull, uint64_t bs, RelayPlan& p) {
     // more than it saves here); past the small-batch limit (k = 3) lane
     // mode takes over from 1/64 of a quad wave of extra blocks on
     const uint64_t k = nfull / quad_slots, extra = nfull % quad_slots;
-    if (lines < 128 || k < relay_min_quad_k() || extra == 0 || extra * 4 > quad_slots ||
+    if (lines < relay_env("CIR_RELAY_QLINES", k == 1 ? 64 : 32) || k < relay_min_quad_k() ||
+        extra == 0 || extra * 4 > quad_slots ||
         (nfull >= quad_small_batch() && extra * 64 > quad_slots))
       return false;
     p.base = nfull - extra;
     p.nrel = extra;
     p.quad = true;
     p.pad = kRelayQuadPad;
-    // beside quad-mode base waves the relayed chain has less slack (none at
-    // k = 1: it is as long as the base's, and every hand-off adds to it), so
-    // longer segments: 16 lines, 32 at k = 1, where it also starts first
-    p.min_seg = k == 1 ? relay_quad1_seg() : 16u;
-    p.relay_first = k == 1;
+    // Beside quad-mode base waves the relay is enqueued first (the base is
+    // short here) with 8-line segments; at k = 1 it has no slack at all (its
+    // chain is as long as the base's and every hand-off adds to it): 32-line
+    // segments (profiles/r02/relay/qshort/)
+    p.min_seg = k == 1 ? relay_quad1_seg()
+                       : (uint32_t)relay_env("CIR_RELAY_QSEG", kRelayMinSegLines);
+    p.relay_first = relay_env("CIR_RELAY_QFIRST", 1) != 0;
   }
   if ((p.nrel + kRelayGroupChains - 1) / kRelayGroupChains > kRelayMaxGroups) return false;
   return true;

@@ -1040,6 +1040,7 @@ RELAY_SHAPES = [
     (16384, "2q", 3000, 99),   # 2 quad waves per SIMD + 3000 chains + a tail
     (65536, "1q", 2, 0),       # 1 quad wave per SIMD + 2 chains
     (32768, "3q", 4, 0),       # past the small-batch limit: quad base of 3 waves
+    (4096, "2q", 77, 3),       # 32-line chains beside 2 quad waves per SIMD
 ]
 
 
@@ -1096,7 +1097,10 @@ def test_relay_rule_bounds(gpu):
     assert f(slots + 1, 2048) == 1
     assert f(qslots - 1, 32768) == 0
     assert f(qslots + 1, 32768) == 1
-    assert f(qslots + 1, 8192) == 0
+    assert f(qslots + 1, 8192) == 1
+    assert f(qslots + 1, 4096) == 0
+    assert f(2 * qslots + 1, 4096) == 1
+    assert f(2 * qslots + 1, 2048) == 0
     assert f(2 * qslots + 1, 32768) == 1
     assert f(2 * qslots + qslots // 4, 32768) == qslots // 4
     assert f(2 * qslots + qslots // 4 + 1, 32768) == 0
