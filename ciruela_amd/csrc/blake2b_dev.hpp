@@ -380,6 +380,34 @@ __device__ __forceinline__ void hash_chain(const uint8_t* p, uint64_t len, uint6
   }
 }
 
+// hash_chain with the next line loaded while the current one compresses
+// (16-byte aligned chains; others take hash_chain): a chain whose wave shares
+// its SIMD with few others no longer waits on memory once per line.  The
+// last line (full or short) goes through load_line_any.
+__device__ __forceinline__ void hash_chain_prefetch(const uint8_t* p, uint64_t len,
+                                                    uint64_t h[8]) {
+  if (reinterpret_cast<uintptr_t>(p) & 15u) {
+    hash_chain(p, len, h);
+    return;
+  }
+  init_state(h);
+  const uint32_t nfull = (uint32_t)(len >> 7);
+  const uint32_t rem = (uint32_t)(len & 127u);
+  const uint32_t total = nfull + ((rem != 0u || len == 0) ? 1u : 0u);
+  const uint32_t nu = total - 1u;  // full lines that are not the last
+  uint64_t ma[16], mb[16];
+  if (nu) load_line16(ma, p);
+  for (uint32_t i = 0; i < nu; i += 2) {
+    if (i + 1u < nu) load_line16(mb, p + ((uint64_t)(i + 1u) << 7));
+    compress(h, ma, (uint64_t)(i + 1u) << 7, false);
+    if (i + 1u >= nu) break;
+    if (i + 2u < nu) load_line16(ma, p + ((uint64_t)(i + 2u) << 7));
+    compress(h, mb, (uint64_t)(i + 2u) << 7, false);
+  }
+  load_line_any(ma, p, nu, nfull, rem, true);
+  compress(h, ma, len, true);
+}
+
 // The first rem (0..128) bytes of a 16-byte aligned line, zero padded, with
 // 16-byte vector loads: a vector that starts below rem is read whole (it
 // lies inside one 16-byte aligned span, so inside the page that holds the

@@ -159,7 +159,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_general(const uint8_t* __restri
 // ---------------------------------------------------------------------------
 // Mixed-length descriptor batch, ordered longest chain first (order.hip):
 // workgroups [0, nq_wg) run quad-per-chain mode (4 lanes per chain, 16 chains
-// per wave, s_setprio 3) over the first min(*n_long, 64 nq_wg) chains; the
+// per wave, s_setprio 3) over the first *n_long chains if <= 64 nq_wg; the
 // rest run lane-per-chain over the remaining ones.  One launch, so the long
 // chains start first and the short ones fill the machine around them.
 // ---------------------------------------------------------------------------
@@ -612,7 +612,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   if (threadIdx.x == 0) flags[g] = 0;
 }
 
-// Quad part of an ordered batch: chains [0, nl), nl = min(*n_long, 64 nq_wg).
+// The chains of an ordered batch that run in quad mode: its long chains when
+// they all fit the quad part (64 nq_wg), none otherwise.  Beyond the quad
+// part's 16384 chains (one exclusive wave per SIMD) the long chains are as
+// many as a lane wave per SIMD can hold or more, and one lane per chain is
+// the faster mode for them (lane mode costs 30 issue slots per chain-line,
+// quad 33); splitting them instead ran the rest in lane mode only after the
+// exclusive quad part had let go of the SIMDs, with the lane workgroups
+// packed onto the CUs that freed first: 256 KiB x 65536 descriptors 31 ms
+// (profiles/r02/desc/).
+__device__ __forceinline__ uint32_t quad_part_chains(uint32_t n_long, uint32_t nq_wg) {
+  return n_long <= nq_wg * 64u ? n_long : 0u;
+}
+
+// Quad part of an ordered batch: chains [0, quad_part_chains()).
 // Latency-bound (one 1 MiB chain = 8192 dependent compressions), so it keeps
 // a line's 40 message words in registers and runs at s_setprio 3; it is its
 // own kernel so the lane part keeps its occupancy.  kExclusive: each wave
@@ -633,7 +646,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))
     if (threadIdx.x == 0) __hip_atomic_fetch_add(n_long + 1, 1u, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
   }
-  const uint32_t nl = min(*n_long, nq_wg * 64u);
+  const uint32_t nl = quad_part_chains(*n_long, nq_wg);
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t first = (blockIdx.x * kWaves + wave) * 16u;
   if (first >= nl) return;
@@ -713,8 +726,11 @@ __device__ __forceinline__ void lane_chain(const uint8_t* __restrict__ arena,
   store_digest(out + (uint64_t)b * 32u, h);
 }
 
-// Unpaced lane part: one lane per chain, one pass (100 VGPRs, 5 waves per
-// SIMD).  With pace != 0 it leaves a paced batch to k_lane_tiles.
+// Unpaced lane part: one lane per chain, one pass, the next line loaded while
+// the current one compresses (hash_chain_prefetch: +2-5 % on lane-only
+// batches, +30 % where few waves share a SIMD; 4 waves per SIMD, ~10 VGPRs
+// spilled around the chain loop, not in it).  With pace != 0 it leaves a
+// paced batch to k_lane_tiles.
 __global__ __launch_bounds__(kThreads, 4) void k_lane_rest(const uint8_t* __restrict__ arena,
                                                             const uint64_t* __restrict__ off,
                                                             const uint32_t* __restrict__ len,
@@ -723,9 +739,13 @@ __global__ __launch_bounds__(kThreads, 4) void k_lane_rest(const uint8_t* __rest
                                                             uint32_t nq_wg, uint32_t pace,
                                                             uint8_t* __restrict__ out) {
   if (lane_paced_wgs(count, nq_wg, pace) != 0) return;
-  const uint32_t nl = min(count[0], nq_wg * 64u);
+  const uint32_t nl = quad_part_chains(count[0], nq_wg);
   const uint64_t j = nl + (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (j < n) lane_chain(arena, off, len, perm[j], out);
+  if (j >= n) return;
+  const uint32_t b = perm[j];
+  uint64_t h[8];
+  hash_chain_prefetch(arena + off[b], len[b], h);
+  store_digest(out + (uint64_t)b * 32u, h);
 }
 
 // Paced lane part (helper == 0): only lane_paced_wgs() workgroups run, and

@@ -88,7 +88,7 @@ hipError_t launch_general_desc(const uint8_t* arena, const uint64_t* off, const 
                                const uint32_t* perm, uint64_t n, uint8_t* out, hipStream_t s);
 
 // Descriptor batch in the order perm (longest chain first); the first
-// min(*n_long, 64 * quad_max_wg(n)) chains (device count) run in quad mode on
+// *n_long chains (device count) run in quad mode when 64 * quad_max_wg(n) hold them, on
 // qs, the rest one lane per chain on `aux`; both fork from s (`fork`) and
 // join back into s (`qjoin`, `ljoin`).
 hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_t* len,

@@ -2,7 +2,8 @@
 path): GiB/s per (block size, block count), one process, HIP events on the
 launch stream.  Run once with CIR_RELAY=0 and once without to A/B the relay
 (k_quad_relay); every shape's digests are compared between the two runs via
-a checksum column.  Diagnostics only (DESIGN.md §5 shapes)."""
+a checksum column.  SWEEP_DESC=1: the same blocks as a descriptor batch
+(cir_hash_blocks_dev).  Diagnostics only (DESIGN.md §5 shapes)."""
 import hashlib
 import os
 import sys
@@ -43,16 +44,27 @@ def main():
     ca._n.check(ca._n.lib.cir_fill_splitmix64_dev(data.data_ptr(), maxb, 0x5EED, 0, 0, stream))
     out = torch.empty(max(n for _, n in SHAPES) * 32, dtype=torch.uint8, device=dev)
     relay = os.environ.get("CIR_RELAY", "1")
+    desc = os.environ.get("SWEEP_DESC") == "1"  # the same blocks as descriptors
     for bs, n in SHAPES:
         nbytes = bs * n
+        if desc:
+            d_off = torch.arange(n, dtype=torch.int64, device=dev) * bs
+            d_len = torch.full((n,), bs, dtype=torch.int32, device=dev)
+
+            def call():
+                ctx.hash_blocks_dev(data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n,
+                                    out.data_ptr(), stream)
+        else:
+            def call():
+                ctx.hash_chunks_dev(data.data_ptr(), nbytes, bs, out.data_ptr(), stream)
         for _ in range(2):
-            ctx.hash_chunks_dev(data.data_ptr(), nbytes, bs, out.data_ptr(), stream)
+            call()
         torch.cuda.synchronize()
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                for _ in range(steps)]
         for a, b in evs:
             a.record()
-            ctx.hash_chunks_dev(data.data_ptr(), nbytes, bs, out.data_ptr(), stream)
+            call()
             b.record()
         torch.cuda.synchronize()
         ms = sorted(a.elapsed_time(b) for a, b in evs)
