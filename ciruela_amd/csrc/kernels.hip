@@ -1050,7 +1050,7 @@ hipError_t launch_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint
 // With k >= 3 lane waves per SIMD the lane part is launched with
 // kRelayLanePad bytes of extra LDS per workgroup: two k_chunks workgroups
 // per CU (2 x 64 KiB of 160), so two lane waves per SIMD (2 x 112 VGPRs)
-// leave room for a relay wave (272) -- three would not.
+// leave room for a relay wave (244) -- three would not.
 constexpr uint32_t kRelayLanePad = 32768;
 // Quad-regime base (k_quad_chunks: 4 waves, 8 KiB static LDS): padded to
 // 81 KiB per workgroup, one workgroup per CU, so one base wave per SIMD
@@ -1108,7 +1108,7 @@ static uint64_t relay_max_k() {
 // caller's stream -- lane mode (k_chunks, quad == false) or quad mode
 // (k_quad_chunks, quad == true) -- and blocks [base, base + nrel) relayed
 // on the quad stream.  `pad`: extra LDS per base workgroup that keeps room
-// for a relay wave (240 VGPRs) on every SIMD.
+// for a relay wave (244 VGPRs) on every SIMD.
 struct RelayPlan {
   uint64_t base = 0, nrel = 0;
   bool quad = false;
@@ -1138,9 +1138,9 @@ static bool relay_plan(uint64_t nfull, uint64_t bs, RelayPlan& p) {
     p.nrel = extra;
     p.pad = k > 2 ? kRelayLanePad : 0u;
   } else {
-    // chains of >= 128 lines only (at 32 lines the relay's hand-offs cost
-    // more than it saves here); past the small-batch limit (k = 3) lane
-    // mode takes over from 1/64 of a quad wave of extra blocks on
+    // short chains cost more hand-offs and launches than they save
+    // (profiles/r02/relay/qshort/); past the small-batch limit (k = 3)
+    // lane mode takes over from 1/64 of a quad wave of extra blocks on
     const uint64_t k = nfull / quad_slots, extra = nfull % quad_slots;
     if (lines < relay_env("CIR_RELAY_QLINES", k == 1 ? 64 : 32) || k < relay_min_quad_k() ||
         extra == 0 || extra * 4 > quad_slots ||
