@@ -500,46 +500,93 @@ __device__ __forceinline__ uint32_t lane_now() {
   return l;
 }
 
-// Segment s of group g from line l0 to the chain's end or l0 + seg_lines.
-// Per-lane addresses are rebuilt from the lane index after each loop, so a
-// relay wave needs no more registers than k_quad_chunks' waves.  max_polls
-// > 0: wait for the predecessor's flag first (0 = the finisher, which does
-// not wait); the segment's first lines are loaded before the wait, so a
-// hand-off costs the flag and the chain value's round trips only.  Returns
-// early (nothing written) when the wait gives up.
-__device__ __forceinline__ void relay_segment(const uint8_t* __restrict__ data, uint64_t bs,
-                                              uint64_t b0, uint32_t nrel, uint32_t g, uint32_t s,
-                                              uint32_t l1_max, uint32_t seg_lines,
-                                              uint32_t* flags, uint64_t* state,
-                                              uint8_t* __restrict__ out, uint8_t* lds,
-                                              uint32_t max_polls, bool publish) {
-  const uint32_t lines = (uint32_t)(bs >> 7);
-  const uint32_t l0 = s * seg_lines, l1 = min(l1_max, lines);
-  const bool final = l1 == lines;
+// The chains a relay hands on, c = 0 .. n-1: the blocks b0 + c of a file
+// of bs-byte blocks (chunk form, every chain the same length) or the chains
+// first + c of an ordered descriptor batch (sorted longest first, so the
+// first chain of a group of 16 is its longest).
+struct RelayFile {
+  const uint8_t* data;
+  uint64_t bs, b0;
+  uint32_t n;
+  __device__ __forceinline__ uint64_t block(uint32_t c) const { return b0 + c; }
+  __device__ __forceinline__ const uint8_t* ptr(uint32_t c) const { return data + (b0 + c) * bs; }
+  __device__ __forceinline__ uint64_t bytes(uint32_t) const { return bs; }
+};
+
+struct RelayDesc {
+  const uint8_t* arena;
+  const uint64_t* off;
+  const uint32_t* len;
+  const uint32_t* perm;
+  uint64_t first;
+  uint32_t n;
+  __device__ __forceinline__ uint64_t block(uint32_t c) const { return perm[first + c]; }
+  __device__ __forceinline__ const uint8_t* ptr(uint32_t c) const { return arena + off[block(c)]; }
+  __device__ __forceinline__ uint64_t bytes(uint32_t c) const { return len[block(c)]; }
+};
+
+// Compressions of a chain of L bytes (the empty input compresses once).
+__device__ __forceinline__ uint32_t chain_lines(uint64_t L) {
+  return L ? (uint32_t)((L + 127u) >> 7) : 1u;
+}
+
+// Segment s of group g: lines [s * seg_lines, l1_max) of each of its chains
+// (clipped to the chain; a chain that ended in an earlier segment sits it
+// out).  Per-lane values are rebuilt from the lane index after each loop, so
+// a relay wave needs no more registers than k_quad_chunks' waves.
+// max_polls > 0: wait for the predecessor's flag first (0 = the finisher,
+// which does not wait); the segment's first lines are loaded before the
+// wait, so a hand-off costs the flag and the chain value's round trips
+// only.  Returns early (nothing written) when the wait gives up, or when
+// the group's chains all ended before this segment (descriptor relays
+// launch the most segments any group can need).
+template <typename R>
+__device__ __forceinline__ void relay_segment(const R& r, uint32_t g, uint32_t s, uint32_t l1_max,
+                                              uint32_t seg_lines, uint32_t* flags,
+                                              uint64_t* state, uint8_t* __restrict__ out,
+                                              uint8_t* lds, uint32_t max_polls, bool publish) {
+  const uint32_t l0 = s * seg_lines;
+  const uint32_t group_lines = chain_lines(r.bytes(g * kRelayGroupChains));
+  if (l0 >= group_lines && s > 0) return;
+  const bool group_final = l1_max >= group_lines;
   auto chain = [&](uint32_t lane) { return g * kRelayGroupChains + (lane >> 2); };
-  const uint32_t n = l1 - l0;
+  // lines of this lane's chain in the segment; nu = the wave's common run
+  // of full, not final, 16-B aligned lines for the hand-scheduled loop
   uint32_t nu = 0;
   if constexpr (CIR_QUAD_FAST && kQuadAsm) {
-    nu = (final ? n - 1u : n) & ~1u;
+    const uint32_t c = chain(lane_now());
+    uint32_t avail = 0xffffffffu;  // quads without a chain here do not bound it
+    if (c < r.n) {
+      const uint64_t L = r.bytes(c);
+      const uint32_t T = chain_lines(L);
+      if (T > l0) {
+        const uint32_t e = min(l1_max, T - 1u);  // the last line is never in the loop
+        const bool al16 = (reinterpret_cast<uintptr_t>(r.ptr(c)) & 15u) == 0;
+        avail = (al16 && e > l0) ? e - l0 : 0u;
+      }
+    }
+    nu = wave_min_u32(avail);
+    nu = nu == 0xffffffffu ? 0u : nu & ~1u;
     if (nu < kQuadFastMin) nu = 0;
   }
+  auto active = [&](uint32_t c) { return c < r.n && chain_lines(r.bytes(c)) > l0; };
   QuadFast f;
   if (nu) {
     const uint32_t lane = lane_now(), c = chain(lane);
-    if (c < nrel) {
+    if (active(c)) {
       uint32_t addr[48];
       quad_addr(addr, (lane >> 2) * 128u, lane & 3u);
-      quad_fast_begin(f, data + (b0 + c) * bs + (uint64_t)l0 * 128u, lds, addr,
-                      (lane >> 2) * 128u, lane & 3u);
+      quad_fast_begin(f, r.ptr(c) + (uint64_t)l0 * 128u, lds, addr, (lane >> 2) * 128u,
+                      lane & 3u);
     }
   }
   if (s > 0 && max_polls) {
     // wait at normal priority (s_sleep: the SIMD's other waves keep issuing)
-    for (uint32_t r = 0;; ++r) {
+    for (uint32_t k = 0;; ++k) {
       const uint32_t fl = __builtin_amdgcn_readfirstlane(
           __hip_atomic_load(flags + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
       if (fl == s) break;
-      if (r >= max_polls) return;  // k_quad_relay_finish takes over from here
+      if (k >= max_polls) return;  // the finisher takes over from here
       __builtin_amdgcn_s_sleep(CIR_RELAY_SLEEP);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -558,31 +605,42 @@ __device__ __forceinline__ void relay_segment(const uint8_t* __restrict__ data, 
   }
   if (nu) {
     const uint32_t lane = lane_now();
-    if (chain(lane) < nrel) quad_fast_run(f, h0, h1, nu, lane & 3u, l0 * 128u);
+    if (active(chain(lane))) quad_fast_run(f, h0, h1, nu, lane & 3u, l0 * 128u);
   }
   {
     const uint32_t lane = lane_now(), c = chain(lane);
-    const bool have = c < nrel;
+    const bool have = active(c);
+    uint64_t L = 0;
+    bool fin = false;
+    const uint8_t* p = nullptr;
+    if (have) {
+      const uint64_t bytes = r.bytes(c);
+      const uint32_t T = chain_lines(bytes);
+      fin = T <= l1_max;
+      const uint64_t t0 = (uint64_t)(l0 + nu) * 128u;
+      L = (fin ? bytes : (uint64_t)min(l1_max, T) * 128u) - t0;
+      p = r.ptr(c) + t0;
+    }
     uint32_t addr[48];
     quad_addr(addr, (lane >> 2) * 128u, lane & 3u);
-    quad_run<true>(h0, h1, (uint64_t)(l0 + nu) * 128u,
-                   data + (have ? (b0 + c) * bs : 0) + (uint64_t)(l0 + nu) * 128u,
-                   have ? (n - nu) * 128u : 0u, have, final, lds, addr, (lane >> 2) * 128u,
-                   lane & 3u);
+    quad_run<true>(h0, h1, (uint64_t)(l0 + nu) * 128u, p, (uint32_t)L, have, fin, lds, addr,
+                   (lane >> 2) * 128u, lane & 3u);
   }
   const uint32_t lane = lane_now(), c = chain(lane);
-  if (final) {
-    if (c < nrel) *reinterpret_cast<uint64_t*>(out + (b0 + c) * 32u + 8u * (lane & 3u)) = h0;
-  } else {
-    uint64_t* st = state + ((uint64_t)g * 64u + lane) * 2u;
-    st[0] = h0;
-    st[1] = h1;
+  if (active(c)) {
+    if (chain_lines(r.bytes(c)) <= l1_max) {
+      *reinterpret_cast<uint64_t*>(out + r.block(c) * 32u + 8u * (lane & 3u)) = h0;
+    } else {
+      uint64_t* st = state + ((uint64_t)g * 64u + lane) * 2u;
+      st[0] = h0;
+      st[1] = h1;
+    }
   }
   if (!publish) return;
   // the chain values (or digests) reach every XCD's view before the flag
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   if (lane == 0)
-    __hip_atomic_store(flags + g, final ? 0xffffffffu : l1 / seg_lines, __ATOMIC_RELAXED,
+    __hip_atomic_store(flags + g, group_final ? 0xffffffffu : s + 1u, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -592,7 +650,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     uint32_t max_polls) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kQuadWaveLds];
   const uint32_t g = blockIdx.x % ngroups, s = blockIdx.x / ngroups;
-  relay_segment(data, bs, b0, nrel, g, s, (s + 1u) * seg_lines, seg_lines, flags, state, out, lds,
+  const RelayFile r{data, bs, b0, nrel};
+  relay_segment(r, g, s, (s + 1u) * seg_lines, seg_lines, flags, state, out, lds,
                 max_polls ? max_polls : 1u, true);
 }
 
@@ -606,9 +665,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   __shared__ __attribute__((aligned(16))) uint8_t lds[kQuadWaveLds];
   const uint32_t g = blockIdx.x;
   const uint32_t s = __builtin_amdgcn_readfirstlane(flags[g]);
+  const RelayFile r{data, bs, b0, nrel};
   if (s != 0xffffffffu)  // else the relay finished this group
-    relay_segment(data, bs, b0, nrel, g, s, 0xffffffffu, seg_lines, flags, state, out, lds, 0u,
-                  false);
+    relay_segment(r, g, s, 0xffffffffu, seg_lines, flags, state, out, lds, 0u, false);
   if (threadIdx.x == 0) flags[g] = 0;
 }
 
@@ -731,17 +790,85 @@ __device__ __forceinline__ void lane_chain(const uint8_t* __restrict__ arena,
 // batches, +30 % where few waves share a SIMD; 4 waves per SIMD, ~10 VGPRs
 // spilled around the chain loop, not in it).  With pace != 0 it leaves a
 // paced batch to k_lane_tiles.
+// Relay of a descriptor batch (launch_mixed): the host launches one when
+// the batch is k = 1 or 2 lane waves per SIMD plus `extra` chains
+// (extra = n mod slots, slots = 64 x SIMDs); whether it runs is decided on
+// the device, where the lengths are: only with no quad part (no long chains,
+// or more than it holds: then every chain is lane mode and extra is exact),
+// when the longest relayed chain (the first of the last `extra`, the order
+// being longest first) has >= 16 lines and extra <= min(1/2, lines/256) of
+// slots (the chunk-form rule, relay_plan, but 1/2 for 5/8: the relay waves
+// on the high-priority stream are dispatched ahead of the lane part and,
+// many of them, keep lane workgroups off the SIMDs: 32 KiB x 106496
+// descriptors 1678 -> 1213 GiB/s with 40960 relayed).  k_lane_rest, the
+// relay and its finisher all evaluate this, so they agree on the split.
+__device__ __forceinline__ bool desc_relay_on(const uint32_t* count, uint32_t nq_wg,
+                                              const uint32_t* len, const uint32_t* perm,
+                                              uint64_t n, uint32_t extra, uint32_t slots) {
+  if (extra == 0 || quad_part_chains(count[0], nq_wg) != 0) return false;
+  const uint64_t lines = chain_lines(len[perm[n - extra]]);
+  return lines >= 16 && (uint64_t)extra * 2 <= (uint64_t)slots &&
+         (uint64_t)extra * 256 <= (uint64_t)slots * lines;
+}
+
+// Segment length of a descriptor relay: at least kRelayMinSegLines, about
+// nseg_max segments for the longest relayed chain.
+__device__ __forceinline__ uint32_t desc_relay_seg(const uint32_t* len, const uint32_t* perm,
+                                                   uint64_t n, uint32_t extra,
+                                                   uint32_t nseg_max) {
+  const uint32_t lines = chain_lines(len[perm[n - extra]]);
+  const uint32_t seg = ((lines + nseg_max - 1u) / nseg_max + 1u) & ~1u;
+  return max(seg, kRelayMinSegLines);
+}
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_desc_relay(
+    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, const uint32_t* __restrict__ perm, uint64_t n,
+    const uint32_t* count, uint32_t nq_wg, uint32_t extra, uint32_t slots, uint32_t ngroups,
+    uint32_t nseg_max, uint32_t polls, uint32_t* flags, uint64_t* state,
+    uint8_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kQuadWaveLds];
+  if (!desc_relay_on(count, nq_wg, len, perm, n, extra, slots)) return;
+  const uint32_t g = blockIdx.x % ngroups, s = blockIdx.x / ngroups;
+  const uint32_t seg = desc_relay_seg(len, perm, n, extra, nseg_max);
+  const RelayDesc r{arena, off, len, perm, n - extra, extra};
+  // polls == 0: the bound from the longest chain (see launch_relay)
+  const uint32_t lines = chain_lines(len[perm[n - extra]]);
+  const uint32_t max_polls = polls ? polls : max(32768u, lines * 64u);
+  relay_segment(r, g, s, (s + 1u) * seg, seg, flags, state, out, lds, max_polls, true);
+}
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_desc_relay_finish(
+    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, const uint32_t* __restrict__ perm, uint64_t n,
+    const uint32_t* count, uint32_t nq_wg, uint32_t extra, uint32_t slots, uint32_t nseg_max,
+    uint32_t* flags, uint64_t* state, uint8_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kQuadWaveLds];
+  if (!desc_relay_on(count, nq_wg, len, perm, n, extra, slots)) return;
+  const uint32_t g = blockIdx.x;
+  const uint32_t s = __builtin_amdgcn_readfirstlane(flags[g]);
+  const uint32_t seg = desc_relay_seg(len, perm, n, extra, nseg_max);
+  const RelayDesc r{arena, off, len, perm, n - extra, extra};
+  if (s != 0xffffffffu)
+    relay_segment(r, g, s, 0xffffffffu, seg, flags, state, out, lds, 0u, false);
+  if (threadIdx.x == 0) flags[g] = 0;
+}
+
 __global__ __launch_bounds__(kThreads, 4) void k_lane_rest(const uint8_t* __restrict__ arena,
                                                             const uint64_t* __restrict__ off,
                                                             const uint32_t* __restrict__ len,
                                                             const uint32_t* __restrict__ perm,
                                                             uint64_t n, const uint32_t* count,
                                                             uint32_t nq_wg, uint32_t pace,
+                                                            uint32_t relay_extra, uint32_t slots,
                                                             uint8_t* __restrict__ out) {
   if (lane_paced_wgs(count, nq_wg, pace) != 0) return;
   const uint32_t nl = quad_part_chains(count[0], nq_wg);
   const uint64_t j = nl + (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (j >= n) return;
+  // the last relay_extra chains are relayed (k_desc_relay) when it runs
+  const uint64_t end =
+      desc_relay_on(count, nq_wg, len, perm, n, relay_extra, slots) ? n - relay_extra : n;
+  if (j >= end) return;
   const uint32_t b = perm[j];
   uint64_t h[8];
   hash_chain_prefetch(arena + off[b], len[b], h);
@@ -1056,6 +1183,9 @@ constexpr uint32_t kRelayLanePad = 32768;
 // 81 KiB per workgroup, one workgroup per CU, so one base wave per SIMD
 // (248 VGPRs) beside a relay wave.
 constexpr uint32_t kRelayQuadPad = 73 * 1024;
+// Descriptor lane part (k_lane_rest, no LDS of its own) beside a relay:
+// two workgroups per CU.
+constexpr uint32_t kRelayDescLanePad = 64 * 1024;
 
 static bool relay_enabled() {
   static const bool on = [] {
@@ -1166,6 +1296,13 @@ uint64_t relay_blocks(uint64_t nfull, uint64_t bs) {
   RelayPlan p;
   return relay_plan(nfull, bs, p) ? p.nrel : 0;
 }
+
+static bool desc_may_relay_slots(uint64_t n, uint64_t slots) {
+  return relay_enabled() && n >= slots && n / slots <= 2 && n % slots != 0 &&
+         (n % slots + kRelayGroupChains - 1) / kRelayGroupChains <= kRelayMaxGroups;
+}
+
+bool desc_may_relay(uint64_t n) { return desc_may_relay_slots(n, 64ull * device_simds()); }
 
 // Blocks [b0, b0 + nrel) of a file of whole bs-byte blocks as relayed quad
 // chains on qs (the relay, then its finisher, which zeroes the flags
@@ -1288,8 +1425,21 @@ static uint32_t lane_pace() {
 hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
                         const uint32_t* perm, uint32_t* n_long, uint64_t n, uint8_t* out,
                         hipStream_t s, hipStream_t qs, hipStream_t aux, hipEvent_t fork,
-                        hipEvent_t qjoin, hipEvent_t ljoin) {
+                        hipEvent_t qjoin, hipEvent_t ljoin, const RelayScratch* relay) {
   if (n == 0) return hipSuccess;
+  // a relay of the chains past k = 1, 2 whole lane waves per SIMD
+  // (desc_relay_on decides on the device whether it runs)
+  const uint64_t slots = 64ull * device_simds();
+  uint32_t extra = 0, groups = 0, nseg_max = 1;
+  if (relay && relay->flags && qs != s && aux != qs && desc_may_relay_slots(n, slots)) {
+    extra = (uint32_t)(n % slots);
+    groups = (extra + kRelayGroupChains - 1) / kRelayGroupChains;
+    if (groups > relay->groups) {
+      extra = 0;
+    } else {
+      nseg_max = (uint32_t)std::max<uint64_t>(1, relay_target_waves(device_simds()) / groups);
+    }
+  }
   const uint64_t nq = std::min<uint64_t>((n + 63) / 64, quad_max_wg(n));
   const uint64_t lane_grid = grid_for(n, kThreads);
   if (lane_grid > 0x7fffffffull) return hipErrorInvalidValue;
@@ -1313,8 +1463,28 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
     if (e != hipSuccess) return e;
     // unpaced batches: k_lane_rest; paced ones: k_lane_tiles (each leaves
     // the other case at once), and the helper behind the quad part
-    hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads), 0, aux, arena, off,
-                       len, perm, n, n_long, (uint32_t)nq, pace, out);
+    if (extra) {
+      // on qs behind the quad part (which is empty whenever the relay runs)
+      uint32_t polls = 0;
+      if (const char* v = getenv("CIR_RELAY_POLLS")) polls = (uint32_t)strtoul(v, nullptr, 10);
+      if (polls == 0 && getenv("CIR_RELAY_POLLS")) polls = 1;  // "0": give up at once
+      hipLaunchKernelGGL(k_desc_relay, dim3(groups * nseg_max), dim3(64), 0, qs, arena, off, len,
+                         perm, n, n_long, (uint32_t)nq, extra, (uint32_t)slots, groups, nseg_max,
+                         polls, relay->flags, relay->state, out);
+      e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(k_desc_relay_finish, dim3(groups), dim3(64), 0, qs, arena, off, len, perm,
+                         n, n_long, (uint32_t)nq, extra, (uint32_t)slots, nseg_max, relay->flags,
+                         relay->state, out);
+      e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    // beside a relay at most two lane waves per SIMD (2 x 128 VGPRs, two
+    // 64 KiB-padded workgroups per CU), so a relay wave (244) always fits;
+    // k <= 2 needs no more
+    hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads),
+                       extra ? kRelayDescLanePad : 0u, aux, arena, off, len, perm, n, n_long,
+                       (uint32_t)nq, pace, extra, (uint32_t)slots, out);
     if (pace != 0) {
       e = hipGetLastError();
       if (e != hipSuccess) return e;
@@ -1327,7 +1497,7 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
     }
   } else {
     hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads), 0, aux, arena, off,
-                       len, perm, n, n_long, (uint32_t)nq, 0u, out);
+                       len, perm, n, n_long, (uint32_t)nq, 0u, 0u, (uint32_t)slots, out);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_quad_long<kQuadAsm, false>), dim3((unsigned)nq), dim3(kThreads), 0, qs,

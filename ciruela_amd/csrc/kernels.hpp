@@ -77,6 +77,9 @@ hipError_t launch_chunks_split(const uint8_t* data, uint64_t nbytes, uint64_t bs
 // Number of blocks launch_chunks_split would relay (0: no relay) for a file
 // of nfull whole blocks of bs bytes on the current device.
 uint64_t relay_blocks(uint64_t nfull, uint64_t bs);
+// Whether launch_mixed may relay the last chains of a descriptor batch of n
+// chains on the current device (1 or 2 lane waves per SIMD and a few more).
+bool desc_may_relay(uint64_t n);
 
 // Blocks first .. first+n-1 of Hashes::hash_file's split of [data, data+nbytes).
 hipError_t launch_general_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs,
@@ -91,10 +94,13 @@ hipError_t launch_general_desc(const uint8_t* arena, const uint64_t* off, const 
 // *n_long chains (device count) run in quad mode when 64 * quad_max_wg(n) hold them, on
 // qs, the rest one lane per chain on `aux`; both fork from s (`fork`) and
 // join back into s (`qjoin`, `ljoin`).
+// relay (nullable): scratch for relaying the chains past k = 1, 2 whole lane
+// waves per SIMD on qs (k_desc_relay; decided on the device).
 hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
                         const uint32_t* perm, uint32_t* n_long, uint64_t n, uint8_t* out,
                         hipStream_t s, hipStream_t qs, hipStream_t aux, hipEvent_t fork,
-                        hipEvent_t qjoin, hipEvent_t ljoin);
+                        hipEvent_t qjoin, hipEvent_t ljoin,
+                        const RelayScratch* relay = nullptr);
 
 // Longest-chain-first order of a descriptor batch (order.hip): *perm points
 // into `scratch` (order_scratch_bytes(n) bytes, device memory).

@@ -184,6 +184,21 @@ static hipError_t create_part_streams(Device& d) {
   return hipStreamCreateWithPriority(&d.qstream, hipStreamNonBlocking, greatest);
 }
 
+// The relay scratch (kernels.hpp RelayScratch), allocated at full capacity
+// on first use: chain values, then the flags, zeroed once on the quad-part
+// stream (each relay's finisher zeroes its groups' flags again).  Caller
+// holds d.order_mu with d's device current and the part streams created.
+int ensure_relay(Device& d) {
+  if (d.relay_mem) return CIR_OK;
+  CIR_HIP(hipMalloc(&d.relay_mem, dev::relay_scratch_bytes(dev::kRelayMaxGroups)));
+  d.relay.state = (uint64_t*)d.relay_mem;
+  d.relay.flags = (uint32_t*)((uint8_t*)d.relay_mem + (size_t)dev::kRelayMaxGroups * 1024u);
+  d.relay.groups = dev::kRelayMaxGroups;
+  CIR_HIP(hipMemsetAsync(d.relay.flags, 0, (size_t)dev::kRelayMaxGroups * 4u,
+                         d.qstream ? d.qstream : d.compute));
+  return CIR_OK;
+}
+
 // The part streams and their events, created on first use (caller holds
 // d.order_mu with d's device current).
 int ensure_part_streams(Device& d) {
@@ -233,6 +248,12 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
     CIR_HIP(hipMalloc(&d.order_scratch, need));
     d.order_cap = need;
   }
+  // a batch of at least one lane wave per SIMD may relay its last chains
+  // (launch_mixed); the SIMD count is the device's
+  if (ht != CIR_HASH_SHA512_256 && d.qstream && dev::desc_may_relay(n)) {
+    rc = ensure_relay(d);
+    if (rc) return rc;
+  }
   CIR_HIP(hipStreamWaitEvent(s, d.order_free, 0));
   uint32_t* perm = nullptr;
   uint32_t* n_long = nullptr;
@@ -241,7 +262,8 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
     CIR_HIP(dev::launch_sha_desc(arena, off, len, perm, n, out, s));
   else
     CIR_HIP(dev::launch_mixed(arena, off, len, perm, n_long, n, out, s, d.qstream ? d.qstream : s,
-                              d.aux ? d.aux : s, d.aux_fork, d.q_join, d.aux_join));
+                              d.aux ? d.aux : s, d.aux_fork, d.q_join, d.aux_join,
+                              d.relay_mem ? &d.relay : nullptr));
   CIR_HIP(hipEventRecord(d.order_free, s));
   return CIR_OK;
 }
@@ -665,16 +687,9 @@ int cir_hash_chunks_dev(cir_ctx* ctx, const void* d_data, uint64_t nbytes, uint6
     CIR_HIP(hipSetDevice(d->id));
     int rc = ensure_part_streams(*d);
     if (rc) return rc;
-    const uint64_t nfull = nbytes / block_size;
-    if (!d->relay_mem && dev::relay_blocks(nfull, block_size) > 0) {
-      // first relayed file on this device: chain values, then the flags
-      const size_t bytes = dev::relay_scratch_bytes(dev::kRelayMaxGroups);
-      CIR_HIP(hipMalloc(&d->relay_mem, bytes));
-      d->relay.state = (uint64_t*)d->relay_mem;
-      d->relay.flags = (uint32_t*)((uint8_t*)d->relay_mem + (size_t)dev::kRelayMaxGroups * 1024u);
-      d->relay.groups = dev::kRelayMaxGroups;
-      // zeroed once; each relay's finisher zeroes its groups' flags again
-      CIR_HIP(hipMemsetAsync(d->relay.flags, 0, (size_t)dev::kRelayMaxGroups * 4u, d->qstream));
+    if (dev::relay_blocks(nbytes / block_size, block_size) > 0) {
+      rc = ensure_relay(*d);
+      if (rc) return rc;
     }
     CIR_HIP(dev::launch_chunks_split((const uint8_t*)d_data, nbytes, block_size, d_out, s,
                                      d->qstream, d->aux_fork, d->q_join, &d->relay));

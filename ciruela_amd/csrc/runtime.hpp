@@ -124,6 +124,7 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
                       uint64_t n, uint8_t* out, hipStream_t s, int ht = CIR_HASH_BLAKE2B_256);
 bool valid_hash_type(int ht);
 int ensure_part_streams(Device& d);
+int ensure_relay(Device& d);
 int slot_wait(Device& d, Slot& s);
 
 }  // namespace cir

@@ -1106,3 +1106,61 @@ def test_relay_rule_bounds(gpu):
     assert f(2 * qslots + qslots // 4 + 1, 32768) == 0
     assert f(3 * qslots + qslots // 64, 32768) == qslots // 64
     assert f(3 * qslots + qslots // 64 + 1, 32768) == 0
+
+
+def desc_batch_check(gpu, ctx, oracle, lens, offs_skew, seed):
+    """Hash lens as a device descriptor batch (offsets 16-B aligned, plus
+    offs_skew(i) bytes) and compare every digest with the oracle."""
+    import torch
+    offs, pos = [], 0
+    for i, ln in enumerate(lens):
+        pos += (-pos) % 16 + offs_skew(i)
+        offs.append(pos)
+        pos += ln
+    data = dev_random(gpu, pos, seed=seed)
+    d_off = torch.tensor(offs, dtype=torch.int64, device="cuda:0")
+    d_len = torch.tensor(lens, dtype=torch.int32, device="cuda:0")
+    out = torch.zeros(32 * len(lens), dtype=torch.uint8, device="cuda:0")
+    for _ in range(2):  # the second call reuses the relay's flags and state
+        ctx.hash_blocks_dev(data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), len(lens),
+                            out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    host = data.cpu().numpy()
+    del data
+    ao = np.array(offs, dtype=np.uint64)
+    al = np.array(lens, dtype=np.uint32)
+    want = np.zeros(32 * len(lens), dtype=np.uint8)
+    oracle.oracle_hash_blocks(host.ctypes.data, ao.ctypes.data, al.ctypes.data, len(lens),
+                              want.ctypes.data, 8)
+    got = out.cpu().numpy()
+    assert first_bad(got, want) is None, "descriptor %s" % first_bad(got, want)
+
+
+@pytest.mark.parametrize("case", ["uniform1", "uniform1000", "ragged", "k2", "longq"])
+@pytest.mark.parametrize("polls", [None, "0"])
+def test_desc_relay(gpu, ctx, oracle, case, polls, monkeypatch):
+    """Descriptor batches of 1 or 2 lane waves per SIMD plus a few chains: the
+    last chains of the order are relayed (k_desc_relay, decided on the
+    device) beside the lane part.  ragged: the relayed chains have mixed
+    lengths (the shortest of the batch: ragged, empty, misaligned starts);
+    longq: a few long chains make a quad part, so no relay runs.  polls "0":
+    the finisher completes every chain."""
+    if polls is not None:
+        monkeypatch.setenv("CIR_RELAY_POLLS", polls)
+    slots = lane_wave_slots()
+    rng = random.Random(hash(case) & 0xffff)
+    skew = lambda i: 0  # noqa: E731
+    if case == "uniform1":
+        lens = [32768] * (slots + 1)
+    elif case == "uniform1000":
+        lens = [32768] * (slots + 1000)
+    elif case == "ragged":
+        lens = [32768] * (slots + 700) + [rng.randrange(0, 32768) for _ in range(77)] + [0, 0, 1]
+        rng.shuffle(lens)
+        skew = lambda i: 5 if i % 13 == 0 else 0  # noqa: E731
+    elif case == "k2":
+        lens = [4096] * (2 * slots + 5000)
+    else:
+        lens = [32768] * (slots + 300) + [1 << 18] * 20
+        rng.shuffle(lens)
+    desc_batch_check(gpu, ctx, oracle, lens, skew, seed=len(lens))
