@@ -525,6 +525,14 @@ struct RelayDesc {
   __device__ __forceinline__ uint64_t bytes(uint32_t c) const { return len[block(c)]; }
 };
 
+// Extra blocks a relay takes at most, as lines / relay_cap_div(lines) of a
+// lane wave per SIMD: at 32-line chains a relay of 1/8 of a wave was no
+// faster than one more lane wave (4 KiB x 73728 / 139264 blocks), so short
+// chains get half the allowance.
+__host__ __device__ __forceinline__ uint64_t relay_cap_div(uint64_t lines) {
+  return lines < 64 ? 512 : 256;
+}
+
 // Compressions of a chain of L bytes (the empty input compresses once).
 __device__ __forceinline__ uint32_t chain_lines(uint64_t L) {
   return L ? (uint32_t)((L + 127u) >> 7) : 1u;
@@ -808,7 +816,7 @@ __device__ __forceinline__ bool desc_relay_on(const uint32_t* count, uint32_t nq
   if (extra == 0 || quad_part_chains(count[0], nq_wg) != 0) return false;
   const uint64_t lines = chain_lines(len[perm[n - extra]]);
   return lines >= 16 && (uint64_t)extra * 2 <= (uint64_t)slots &&
-         (uint64_t)extra * 256 <= (uint64_t)slots * lines;
+         (uint64_t)extra * relay_cap_div(lines) <= (uint64_t)slots * lines;
 }
 
 // Segment length of a descriptor relay: at least kRelayMinSegLines, about
@@ -1249,7 +1257,7 @@ struct RelayPlan {
 
 // Lane regime (nfull >= one lane wave per SIMD): k = 1 .. CIR_RELAY_MAXK whole
 // lane waves per SIMD plus extra blocks up to min(5/8, lines/256) of a lane
-// wave per SIMD; beyond that one more lane wave (or the quad band of
+// wave per SIMD (lines/512 below 64 lines); beyond that one more lane wave (or the quad band of
 // chunks_in_quad) costs less than the relayed chains' quad-mode work
 // (profiles/r02/relay/).  Quad regime (below one lane wave per SIMD):
 // k >= 1 whole quad waves per SIMD plus up to 1/4 of one (1/64 past the
@@ -1262,7 +1270,7 @@ static bool relay_plan(uint64_t nfull, uint64_t bs, RelayPlan& p) {
   const uint64_t lane_slots = 64ull * simds, quad_slots = 16ull * simds;
   if (nfull >= lane_slots) {
     const uint64_t k = nfull / lane_slots, extra = nfull % lane_slots;
-    const uint64_t cap = std::min(lane_slots * 5 / 8, lane_slots * lines / 256);
+    const uint64_t cap = std::min(lane_slots * 5 / 8, lane_slots * lines / relay_cap_div(lines));
     if (k > relay_max_k() || extra == 0 || extra > cap) return false;
     p.base = nfull - extra;
     p.nrel = extra;

@@ -1032,8 +1032,8 @@ def lane_wave_slots():
 RELAY_SHAPES = [
     (32768, 1, 1, 0),          # one extra chain: 16 segments of 16 lines
     (32768, 1, 1000, 777),     # 63 groups + the short last block beside
-    (4096, 2, 5000, 1),        # k = 2, 32-line chains: 2 segments each
-    (2048, 1, 4000, 0),        # 250 groups of 16-line chains: one segment each
+    (4096, 2, 4000, 1),        # k = 2, 32-line chains: 4 segments each
+    (2048, 1, 2000, 0),        # 125 groups of 16-line chains: 2 segments each
     (131072, 1, 3, 0),         # 1024-line chains: 64 segments
     (4096, 4, 100, 5),         # k >= 3: the lane part with padded LDS (2 waves per SIMD)
     (32768, "2q", 1, 0),       # quad regime: 2 quad waves per SIMD + 1 chain
@@ -1077,7 +1077,8 @@ def test_chunks_dev_relay(gpu, ctx, oracle, bs, k, extra, tail, polls, monkeypat
 
 def test_relay_rule_bounds(gpu):
     """No relay below one quad wave per SIMD, beyond k = 16 lane waves, past
-    5/8 of a lane wave (lines / 256 for short chains) or 1/4 of a quad wave
+    5/8 of a lane wave (lines / 256 for short chains, lines / 512 below 64
+    lines) or 1/4 of a quad wave
     (1/64 past the small-batch limit) of extra blocks, below 16 lines, or in
     the quad regime below 128 lines."""
     slots = lane_wave_slots()
@@ -1091,8 +1092,9 @@ def test_relay_rule_bounds(gpu):
     assert f(17 * slots + 1, 32768) == 0
     assert f(slots + slots * 5 // 8, 32768) == slots * 5 // 8
     assert f(slots + slots * 5 // 8 + 1, 32768) == 0
-    assert f(slots + slots // 8, 4096) == slots // 8
-    assert f(slots + slots // 8 + 1, 4096) == 0
+    assert f(slots + slots // 16, 4096) == slots // 16
+    assert f(slots + slots // 16 + 1, 4096) == 0
+    assert f(slots + slots // 4, 8192) == slots // 4
     assert f(slots + 1, 1024) == 0
     assert f(slots + 1, 2048) == 1
     assert f(qslots - 1, 32768) == 0
@@ -1159,7 +1161,7 @@ def test_desc_relay(gpu, ctx, oracle, case, polls, monkeypatch):
         rng.shuffle(lens)
         skew = lambda i: 5 if i % 13 == 0 else 0  # noqa: E731
     elif case == "k2":
-        lens = [4096] * (2 * slots + 5000)
+        lens = [4096] * (2 * slots + 4000)
     else:
         lens = [32768] * (slots + 300) + [1 << 18] * 20
         rng.shuffle(lens)
