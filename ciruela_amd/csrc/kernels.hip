@@ -692,17 +692,34 @@ __device__ __forceinline__ uint32_t quad_part_chains(uint32_t n_long, uint32_t n
   return n_long <= nq_wg * 64u ? n_long : 0u;
 }
 
+// Relay of a small descriptor batch (quad regime, launch_mixed): the host
+// launches one when n = 16384 k + extra (16 chains per quad wave, one wave
+// per SIMD per k), extra <= 1/4 of that; it runs only when every chain of
+// the batch is in the quad part (count[0] == n, so the split is exact) and
+// the longest relayed chain has >= min_lines lines (the chunk-form rule:
+// 64 at k = 1, 32 above).
+__device__ __forceinline__ bool desc_qrelay_on(const uint32_t* count, const uint32_t* len,
+                                               const uint32_t* perm, uint64_t n, uint32_t extra,
+                                               uint32_t min_lines) {
+  if (extra == 0 || min_lines == 0 || count[0] != n) return false;
+  return chain_lines(len[perm[n - extra]]) >= min_lines;
+}
+
 // Quad part of an ordered batch: chains [0, quad_part_chains()).
 // Latency-bound (one 1 MiB chain = 8192 dependent compressions), so it keeps
 // a line's 40 message words in registers and runs at s_setprio 3; it is its
 // own kernel so the lane part keeps its occupancy.  kExclusive: each wave
 // touches a255, so it holds the SIMD's whole 512-register file and no lane
 // wave can share its SIMD (batches with a lane part beside the quad part).
+// relay_extra / relay_min_lines (small batches only): the last relay_extra
+// chains run in k_desc_relay instead when desc_qrelay_on (the base then
+// runs at priority 2 so the relay's segments issue first).
 template <bool kAsm, bool kExclusive>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_quad_long(
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ perm, uint32_t* n_long,
-    uint32_t nq_wg, uint8_t* __restrict__ out) {
+    uint32_t nq_wg, uint8_t* __restrict__ out, uint64_t n, uint32_t relay_extra,
+    uint32_t relay_min_lines) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWaves * kQuadWaveLds];
 #ifdef CIR_QPAD  // code-layout probe: CIR_QPAD 4-byte s_nop's ahead of the body
   asm volatile(".rept " CIR_STR(CIR_QPAD) "\ns_nop 0\n.endr");
@@ -713,11 +730,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))
     if (threadIdx.x == 0) __hip_atomic_fetch_add(n_long + 1, 1u, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
   }
-  const uint32_t nl = quad_part_chains(*n_long, nq_wg);
+  const bool relayed = desc_qrelay_on(n_long, len, perm, n, relay_extra, relay_min_lines);
+  const uint32_t nl = relayed ? (uint32_t)(n - relay_extra) : quad_part_chains(*n_long, nq_wg);
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t first = (blockIdx.x * kWaves + wave) * 16u;
   if (first >= nl) return;
-  __builtin_amdgcn_s_setprio(3);
+  if (relayed)
+    __builtin_amdgcn_s_setprio(2);
+  else
+    __builtin_amdgcn_s_setprio(3);
 #ifdef CIR_QUAD_CLOCK  // diagnostics build: per-wave shader clock / 100 MHz clock
   const uint64_t c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -819,26 +840,36 @@ __device__ __forceinline__ bool desc_relay_on(const uint32_t* count, uint32_t nq
          (uint64_t)extra * relay_cap_div(lines) <= (uint64_t)slots * lines;
 }
 
-// Segment length of a descriptor relay: at least kRelayMinSegLines, about
+// Segment length of a descriptor relay: at least min_seg lines, about
 // nseg_max segments for the longest relayed chain.
 __device__ __forceinline__ uint32_t desc_relay_seg(const uint32_t* len, const uint32_t* perm,
-                                                   uint64_t n, uint32_t extra,
-                                                   uint32_t nseg_max) {
+                                                   uint64_t n, uint32_t extra, uint32_t nseg_max,
+                                                   uint32_t min_seg) {
   const uint32_t lines = chain_lines(len[perm[n - extra]]);
   const uint32_t seg = ((lines + nseg_max - 1u) / nseg_max + 1u) & ~1u;
-  return max(seg, kRelayMinSegLines);
+  return max(seg, min_seg);
+}
+
+// Lane regime (qmin == 0: desc_relay_on) or quad regime (qmin = the
+// shortest chain worth relaying: desc_qrelay_on).
+__device__ __forceinline__ bool desc_any_relay_on(const uint32_t* count, uint32_t nq_wg,
+                                                  const uint32_t* len, const uint32_t* perm,
+                                                  uint64_t n, uint32_t extra, uint32_t slots,
+                                                  uint32_t qmin) {
+  return qmin ? desc_qrelay_on(count, len, perm, n, extra, qmin)
+              : desc_relay_on(count, nq_wg, len, perm, n, extra, slots);
 }
 
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_desc_relay(
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ perm, uint64_t n,
     const uint32_t* count, uint32_t nq_wg, uint32_t extra, uint32_t slots, uint32_t ngroups,
-    uint32_t nseg_max, uint32_t polls, uint32_t* flags, uint64_t* state,
-    uint8_t* __restrict__ out) {
+    uint32_t nseg_max, uint32_t polls, uint32_t qmin, uint32_t min_seg, uint32_t* flags,
+    uint64_t* state, uint8_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kQuadWaveLds];
-  if (!desc_relay_on(count, nq_wg, len, perm, n, extra, slots)) return;
+  if (!desc_any_relay_on(count, nq_wg, len, perm, n, extra, slots, qmin)) return;
   const uint32_t g = blockIdx.x % ngroups, s = blockIdx.x / ngroups;
-  const uint32_t seg = desc_relay_seg(len, perm, n, extra, nseg_max);
+  const uint32_t seg = desc_relay_seg(len, perm, n, extra, nseg_max, min_seg);
   const RelayDesc r{arena, off, len, perm, n - extra, extra};
   // polls == 0: the bound from the longest chain (see launch_relay)
   const uint32_t lines = chain_lines(len[perm[n - extra]]);
@@ -850,12 +881,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ perm, uint64_t n,
     const uint32_t* count, uint32_t nq_wg, uint32_t extra, uint32_t slots, uint32_t nseg_max,
-    uint32_t* flags, uint64_t* state, uint8_t* __restrict__ out) {
+    uint32_t qmin, uint32_t min_seg, uint32_t* flags, uint64_t* state,
+    uint8_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kQuadWaveLds];
-  if (!desc_relay_on(count, nq_wg, len, perm, n, extra, slots)) return;
+  if (!desc_any_relay_on(count, nq_wg, len, perm, n, extra, slots, qmin)) return;
   const uint32_t g = blockIdx.x;
   const uint32_t s = __builtin_amdgcn_readfirstlane(flags[g]);
-  const uint32_t seg = desc_relay_seg(len, perm, n, extra, nseg_max);
+  const uint32_t seg = desc_relay_seg(len, perm, n, extra, nseg_max, min_seg);
   const RelayDesc r{arena, off, len, perm, n - extra, extra};
   if (s != 0xffffffffu)
     relay_segment(r, g, s, 0xffffffffu, seg, flags, state, out, lds, 0u, false);
@@ -1310,7 +1342,12 @@ static bool desc_may_relay_slots(uint64_t n, uint64_t slots) {
          (n % slots + kRelayGroupChains - 1) / kRelayGroupChains <= kRelayMaxGroups;
 }
 
-bool desc_may_relay(uint64_t n) { return desc_may_relay_slots(n, 64ull * device_simds()); }
+bool desc_may_relay(uint64_t n) {
+  const uint64_t qslots = 16ull * device_simds();
+  const bool quad_regime = relay_enabled() && n < quad_small_batch() && n >= qslots &&
+                           n % qslots != 0 && (n % qslots) * 4 <= qslots;
+  return quad_regime || desc_may_relay_slots(n, 64ull * device_simds());
+}
 
 // Blocks [b0, b0 + nrel) of a file of whole bs-byte blocks as relayed quad
 // chains on qs (the relay, then its finisher, which zeroes the flags
@@ -1430,6 +1467,28 @@ static uint32_t lane_pace() {
   return pace;
 }
 
+// The descriptor relay (k_desc_relay + its finisher) of the last `extra`
+// chains of an ordered batch on stream st; the kernels decide on the device
+// whether it runs (qmin == 0: lane regime, else quad regime).
+static hipError_t launch_desc_relay(const uint8_t* arena, const uint64_t* off,
+                                    const uint32_t* len, const uint32_t* perm, uint64_t n,
+                                    uint32_t* n_long, uint32_t nq, uint32_t extra,
+                                    uint32_t slots, uint32_t groups, uint32_t nseg_max,
+                                    uint32_t qmin, uint32_t min_seg, const RelayScratch& r,
+                                    uint8_t* out, hipStream_t st) {
+  uint32_t polls = 0;  // 0: the device's bound; CIR_RELAY_POLLS=0: give up at once
+  if (const char* v = getenv("CIR_RELAY_POLLS"))
+    polls = std::max(1u, (uint32_t)strtoul(v, nullptr, 10));
+  hipLaunchKernelGGL(k_desc_relay, dim3(groups * nseg_max), dim3(64), 0, st, arena, off, len,
+                     perm, n, n_long, nq, extra, slots, groups, nseg_max, polls, qmin, min_seg,
+                     r.flags, r.state, out);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_desc_relay_finish, dim3(groups), dim3(64), 0, st, arena, off, len, perm, n,
+                     n_long, nq, extra, slots, nseg_max, qmin, min_seg, r.flags, r.state, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
                         const uint32_t* perm, uint32_t* n_long, uint64_t n, uint8_t* out,
                         hipStream_t s, hipStream_t qs, hipStream_t aux, hipEvent_t fork,
@@ -1463,7 +1522,7 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
     // hold their CUs (k_gate), so its waves fill the other CUs instead of
     // taking every SIMD first.
     hipLaunchKernelGGL((k_quad_long<kQuadAsm, true>), dim3((unsigned)nq), dim3(kThreads), 0, qs,
-                       arena, off, len, perm, n_long, (uint32_t)nq, out);
+                       arena, off, len, perm, n_long, (uint32_t)nq, out, n, 0u, 0u);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, aux, n_long + 1, (uint32_t)nq, 600u);
@@ -1473,18 +1532,9 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
     // the other case at once), and the helper behind the quad part
     if (extra) {
       // on qs behind the quad part (which is empty whenever the relay runs)
-      uint32_t polls = 0;
-      if (const char* v = getenv("CIR_RELAY_POLLS")) polls = (uint32_t)strtoul(v, nullptr, 10);
-      if (polls == 0 && getenv("CIR_RELAY_POLLS")) polls = 1;  // "0": give up at once
-      hipLaunchKernelGGL(k_desc_relay, dim3(groups * nseg_max), dim3(64), 0, qs, arena, off, len,
-                         perm, n, n_long, (uint32_t)nq, extra, (uint32_t)slots, groups, nseg_max,
-                         polls, relay->flags, relay->state, out);
-      e = hipGetLastError();
-      if (e != hipSuccess) return e;
-      hipLaunchKernelGGL(k_desc_relay_finish, dim3(groups), dim3(64), 0, qs, arena, off, len, perm,
-                         n, n_long, (uint32_t)nq, extra, (uint32_t)slots, nseg_max, relay->flags,
-                         relay->state, out);
-      e = hipGetLastError();
+      e = launch_desc_relay(arena, off, len, perm, n, n_long, (uint32_t)nq, extra,
+                            (uint32_t)slots, groups, nseg_max, 0u, kRelayMinSegLines, *relay, out,
+                            qs);
       if (e != hipSuccess) return e;
     }
     // beside a relay at most two lane waves per SIMD (2 x 128 VGPRs, two
@@ -1504,12 +1554,32 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
                          off, len, perm, n, n_long, (uint32_t)nq, pace, 1u, out);
     }
   } else {
+    // small batch: a relay of the chains past k whole quad waves per SIMD
+    // on the lane part's stream (aux; the caller's stream by default) beside
+    // the quad part on qs (desc_qrelay_on decides on the device), whose
+    // workgroups are then padded to one per CU to leave room for it
+    const uint64_t qslots = 16ull * device_simds();
+    uint32_t qextra = 0, qmin = 0;
+    if (relay && relay->flags && relay_enabled() && aux != qs && n >= qslots &&
+        n % qslots != 0 && (n % qslots) * 4 <= qslots) {
+      qextra = (uint32_t)(n % qslots);
+      const uint32_t qgroups = (qextra + kRelayGroupChains - 1) / kRelayGroupChains;
+      const uint32_t qk = (uint32_t)(n / qslots);
+      qmin = qk == 1 ? 64u : 32u;
+      const uint32_t qnseg =
+          (uint32_t)std::max<uint64_t>(1, relay_target_waves(device_simds()) / qgroups);
+      e = launch_desc_relay(arena, off, len, perm, n, n_long, (uint32_t)nq, qextra,
+                            (uint32_t)qslots, qgroups, qnseg, qmin,
+                            qk == 1 ? relay_quad1_seg() : kRelayMinSegLines, *relay, out, aux);
+      if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads), 0, aux, arena, off,
                        len, perm, n, n_long, (uint32_t)nq, 0u, 0u, (uint32_t)slots, out);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_quad_long<kQuadAsm, false>), dim3((unsigned)nq), dim3(kThreads), 0, qs,
-                       arena, off, len, perm, n_long, (uint32_t)nq, out);
+    hipLaunchKernelGGL((k_quad_long<kQuadAsm, false>), dim3((unsigned)nq), dim3(kThreads),
+                       qextra ? kRelayQuadPad : 0u, qs, arena, off, len, perm, n_long,
+                       (uint32_t)nq, out, n, qextra, qmin);
   }
   e = hipGetLastError();
   if (e == hipSuccess && qs != s) e = hipEventRecord(qjoin, qs);

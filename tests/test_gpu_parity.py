@@ -1138,18 +1138,22 @@ def desc_batch_check(gpu, ctx, oracle, lens, offs_skew, seed):
     assert first_bad(got, want) is None, "descriptor %s" % first_bad(got, want)
 
 
-@pytest.mark.parametrize("case", ["uniform1", "uniform1000", "ragged", "k2", "longq"])
+@pytest.mark.parametrize("case", ["uniform1", "uniform1000", "ragged", "k2", "longq",
+                                  "q1", "q2", "q2ragged", "q2short", "qmixed"])
 @pytest.mark.parametrize("polls", [None, "0"])
 def test_desc_relay(gpu, ctx, oracle, case, polls, monkeypatch):
     """Descriptor batches of 1 or 2 lane waves per SIMD plus a few chains: the
     last chains of the order are relayed (k_desc_relay, decided on the
     device) beside the lane part.  ragged: the relayed chains have mixed
     lengths (the shortest of the batch: ragged, empty, misaligned starts);
-    longq: a few long chains make a quad part, so no relay runs.  polls "0":
-    the finisher completes every chain."""
+    longq: a few long chains make a quad part, so no relay runs.  q*: small
+    batches (quad regime: k whole quad waves per SIMD plus a few chains,
+    relayed beside the quad part); qmixed has chains below 8 lines, so no
+    relay runs.  polls "0": the finisher completes every chain."""
     if polls is not None:
         monkeypatch.setenv("CIR_RELAY_POLLS", polls)
     slots = lane_wave_slots()
+    qslots = slots // 4
     rng = random.Random(hash(case) & 0xffff)
     skew = lambda i: 0  # noqa: E731
     if case == "uniform1":
@@ -1162,7 +1166,20 @@ def test_desc_relay(gpu, ctx, oracle, case, polls, monkeypatch):
         skew = lambda i: 5 if i % 13 == 0 else 0  # noqa: E731
     elif case == "k2":
         lens = [4096] * (2 * slots + 4000)
-    else:
+    elif case == "longq":
         lens = [32768] * (slots + 300) + [1 << 18] * 20
+        rng.shuffle(lens)
+    elif case == "q1":
+        lens = [65536] * (qslots + 2)
+    elif case == "q2":
+        lens = [32768] * (2 * qslots + 1)
+    elif case == "q2ragged":
+        lens = [32768] * (2 * qslots + 250) + [rng.randrange(1024, 32768) for _ in range(50)]
+        rng.shuffle(lens)
+        skew = lambda i: 3 if i % 17 == 0 else 0  # noqa: E731
+    elif case == "q2short":
+        lens = [4096] * (2 * qslots + 999)
+    else:
+        lens = [32768] * (2 * qslots + 100) + [rng.randrange(0, 1000) for _ in range(10)]
         rng.shuffle(lens)
     desc_batch_check(gpu, ctx, oracle, lens, skew, seed=len(lens))
