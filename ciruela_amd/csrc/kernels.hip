@@ -820,7 +820,7 @@ __device__ __forceinline__ void lane_chain(const uint8_t* __restrict__ arena,
 // spilled around the chain loop, not in it).  With pace != 0 it leaves a
 // paced batch to k_lane_tiles.
 // Relay of a descriptor batch (launch_mixed): the host launches one when
-// the batch is k = 1 or 2 lane waves per SIMD plus `extra` chains
+// the batch is k = 1 .. CIR_RELAY_MAXK lane waves per SIMD plus `extra` chains
 // (extra = n mod slots, slots = 64 x SIMDs); whether it runs is decided on
 // the device, where the lengths are: only with no quad part (no long chains,
 // or more than it holds: then every chain is lane mode and extra is exact),
@@ -1338,7 +1338,7 @@ uint64_t relay_blocks(uint64_t nfull, uint64_t bs) {
 }
 
 static bool desc_may_relay_slots(uint64_t n, uint64_t slots) {
-  return relay_enabled() && n >= slots && n / slots <= 2 && n % slots != 0 &&
+  return relay_enabled() && n >= slots && n / slots <= relay_max_k() && n % slots != 0 &&
          (n % slots + kRelayGroupChains - 1) / kRelayGroupChains <= kRelayMaxGroups;
 }
 
@@ -1494,8 +1494,8 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
                         hipStream_t s, hipStream_t qs, hipStream_t aux, hipEvent_t fork,
                         hipEvent_t qjoin, hipEvent_t ljoin, const RelayScratch* relay) {
   if (n == 0) return hipSuccess;
-  // a relay of the chains past k = 1, 2 whole lane waves per SIMD
-  // (desc_relay_on decides on the device whether it runs)
+  // a relay of the chains past k whole lane waves per SIMD (desc_relay_on
+  // decides on the device whether it runs)
   const uint64_t slots = 64ull * device_simds();
   uint32_t extra = 0, groups = 0, nseg_max = 1;
   if (relay && relay->flags && qs != s && aux != qs && desc_may_relay_slots(n, slots)) {
@@ -1539,7 +1539,7 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
     }
     // beside a relay at most two lane waves per SIMD (2 x 128 VGPRs, two
     // 64 KiB-padded workgroups per CU), so a relay wave (244) always fits;
-    // k <= 2 needs no more
+    // the lane body is issue-bound, two waves per SIMD run it as fast
     hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads),
                        extra ? kRelayDescLanePad : 0u, aux, arena, off, len, perm, n, n_long,
                        (uint32_t)nq, pace, extra, (uint32_t)slots, out);

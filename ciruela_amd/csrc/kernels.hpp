@@ -68,7 +68,7 @@ inline size_t relay_scratch_bytes(uint32_t groups) { return (size_t)groups * (4 
 
 // launch_chunks with the ragged rest in quad mode on qs, concurrently with
 // the uniform part on s (fork / join events); a file of k whole lane waves
-// per SIMD plus a few blocks (k = 1, 2) runs the extra blocks as relayed
+// per SIMD plus a few blocks runs the extra blocks as relayed
 // quad chains on qs (relay, when given); launch_chunks where neither
 // applies (small or misaligned files, no rest, qs null or == s).
 hipError_t launch_chunks_split(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint8_t* out,
@@ -78,7 +78,7 @@ hipError_t launch_chunks_split(const uint8_t* data, uint64_t nbytes, uint64_t bs
 // of nfull whole blocks of bs bytes on the current device.
 uint64_t relay_blocks(uint64_t nfull, uint64_t bs);
 // Whether launch_mixed may relay the last chains of a descriptor batch of n
-// chains on the current device (1 or 2 lane waves per SIMD and a few more,
+// chains on the current device (1 .. 16 lane waves per SIMD and a few more,
 // or a small batch of whole quad waves per SIMD and a few more).
 bool desc_may_relay(uint64_t n);
 
@@ -95,8 +95,8 @@ hipError_t launch_general_desc(const uint8_t* arena, const uint64_t* off, const 
 // *n_long chains (device count) run in quad mode when 64 * quad_max_wg(n) hold them, on
 // qs, the rest one lane per chain on `aux`; both fork from s (`fork`) and
 // join back into s (`qjoin`, `ljoin`).
-// relay (nullable): scratch for relaying the chains past k = 1, 2 whole lane
-// waves per SIMD on qs (k_desc_relay; decided on the device).
+// relay (nullable): scratch for relaying the chains past k whole lane (or
+// quad) waves per SIMD (k_desc_relay; decided on the device).
 hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
                         const uint32_t* perm, uint32_t* n_long, uint64_t n, uint8_t* out,
                         hipStream_t s, hipStream_t qs, hipStream_t aux, hipEvent_t fork,

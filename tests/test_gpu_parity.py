@@ -1138,11 +1138,11 @@ def desc_batch_check(gpu, ctx, oracle, lens, offs_skew, seed):
     assert first_bad(got, want) is None, "descriptor %s" % first_bad(got, want)
 
 
-@pytest.mark.parametrize("case", ["uniform1", "uniform1000", "ragged", "k2", "longq",
+@pytest.mark.parametrize("case", ["uniform1", "uniform1000", "ragged", "k2", "k4", "longq",
                                   "q1", "q2", "q2ragged", "q2short", "qmixed"])
 @pytest.mark.parametrize("polls", [None, "0"])
 def test_desc_relay(gpu, ctx, oracle, case, polls, monkeypatch):
-    """Descriptor batches of 1 or 2 lane waves per SIMD plus a few chains: the
+    """Descriptor batches of k lane waves per SIMD plus a few chains: the
     last chains of the order are relayed (k_desc_relay, decided on the
     device) beside the lane part.  ragged: the relayed chains have mixed
     lengths (the shortest of the batch: ragged, empty, misaligned starts);
@@ -1166,6 +1166,8 @@ def test_desc_relay(gpu, ctx, oracle, case, polls, monkeypatch):
         skew = lambda i: 5 if i % 13 == 0 else 0  # noqa: E731
     elif case == "k2":
         lens = [4096] * (2 * slots + 4000)
+    elif case == "k4":  # the lane part padded to two waves per SIMD beside the relay
+        lens = [8192] * (4 * slots + 1500)
     elif case == "longq":
         lens = [32768] * (slots + 300) + [1 << 18] * 20
         rng.shuffle(lens)
