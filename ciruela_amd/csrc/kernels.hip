@@ -825,18 +825,20 @@ __device__ __forceinline__ void lane_chain(const uint8_t* __restrict__ arena,
 // the device, where the lengths are: only with no quad part (no long chains,
 // or more than it holds: then every chain is lane mode and extra is exact),
 // when the longest relayed chain (the first of the last `extra`, the order
-// being longest first) has >= 16 lines and extra <= min(1/2, lines/256) of
-// slots (the chunk-form rule, relay_plan, but 1/2 for 5/8: the relay waves
-// on the high-priority stream are dispatched ahead of the lane part and,
-// many of them, keep lane workgroups off the SIMDs: 32 KiB x 106496
-// descriptors 1678 -> 1213 GiB/s with 40960 relayed).  k_lane_rest, the
-// relay and its finisher all evaluate this, so they agree on the split.
+// being longest first) has >= 16 lines and extra <= min(cap8 / 8, lines /
+// 256) of slots (the chunk-form rule, relay_plan; cap8 = 5).  The relay
+// waves go in behind a gate on the lane part's workgroups (launch_mixed):
+// without it they were dispatched first, on the high-priority stream, and
+// kept lane workgroups off the SIMDs (32 KiB x 106496 descriptors 1678 ->
+// 1213 GiB/s with 40960 relayed).  k_lane_rest, the relay and its finisher
+// all evaluate this, so they agree on the split.
 __device__ __forceinline__ bool desc_relay_on(const uint32_t* count, uint32_t nq_wg,
                                               const uint32_t* len, const uint32_t* perm,
-                                              uint64_t n, uint32_t extra, uint32_t slots) {
+                                              uint64_t n, uint32_t extra, uint32_t slots,
+                                              uint32_t cap8) {
   if (extra == 0 || quad_part_chains(count[0], nq_wg) != 0) return false;
   const uint64_t lines = chain_lines(len[perm[n - extra]]);
-  return lines >= 16 && (uint64_t)extra * 2 <= (uint64_t)slots &&
+  return lines >= 16 && (uint64_t)extra * 8 <= (uint64_t)slots * cap8 &&
          (uint64_t)extra * relay_cap_div(lines) <= (uint64_t)slots * lines;
 }
 
@@ -855,19 +857,19 @@ __device__ __forceinline__ uint32_t desc_relay_seg(const uint32_t* len, const ui
 __device__ __forceinline__ bool desc_any_relay_on(const uint32_t* count, uint32_t nq_wg,
                                                   const uint32_t* len, const uint32_t* perm,
                                                   uint64_t n, uint32_t extra, uint32_t slots,
-                                                  uint32_t qmin) {
+                                                  uint32_t qmin, uint32_t cap8) {
   return qmin ? desc_qrelay_on(count, len, perm, n, extra, qmin)
-              : desc_relay_on(count, nq_wg, len, perm, n, extra, slots);
+              : desc_relay_on(count, nq_wg, len, perm, n, extra, slots, cap8);
 }
 
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_desc_relay(
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ perm, uint64_t n,
     const uint32_t* count, uint32_t nq_wg, uint32_t extra, uint32_t slots, uint32_t ngroups,
-    uint32_t nseg_max, uint32_t polls, uint32_t qmin, uint32_t min_seg, uint32_t* flags,
-    uint64_t* state, uint8_t* __restrict__ out) {
+    uint32_t nseg_max, uint32_t polls, uint32_t qmin, uint32_t min_seg, uint32_t cap8,
+    uint32_t* flags, uint64_t* state, uint8_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kQuadWaveLds];
-  if (!desc_any_relay_on(count, nq_wg, len, perm, n, extra, slots, qmin)) return;
+  if (!desc_any_relay_on(count, nq_wg, len, perm, n, extra, slots, qmin, cap8)) return;
   const uint32_t g = blockIdx.x % ngroups, s = blockIdx.x / ngroups;
   const uint32_t seg = desc_relay_seg(len, perm, n, extra, nseg_max, min_seg);
   const RelayDesc r{arena, off, len, perm, n - extra, extra};
@@ -881,10 +883,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ perm, uint64_t n,
     const uint32_t* count, uint32_t nq_wg, uint32_t extra, uint32_t slots, uint32_t nseg_max,
-    uint32_t qmin, uint32_t min_seg, uint32_t* flags, uint64_t* state,
+    uint32_t qmin, uint32_t min_seg, uint32_t cap8, uint32_t* flags, uint64_t* state,
     uint8_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kQuadWaveLds];
-  if (!desc_any_relay_on(count, nq_wg, len, perm, n, extra, slots, qmin)) return;
+  if (!desc_any_relay_on(count, nq_wg, len, perm, n, extra, slots, qmin, cap8)) return;
   const uint32_t g = blockIdx.x;
   const uint32_t s = __builtin_amdgcn_readfirstlane(flags[g]);
   const uint32_t seg = desc_relay_seg(len, perm, n, extra, nseg_max, min_seg);
@@ -898,16 +900,21 @@ __global__ __launch_bounds__(kThreads, 4) void k_lane_rest(const uint8_t* __rest
                                                             const uint64_t* __restrict__ off,
                                                             const uint32_t* __restrict__ len,
                                                             const uint32_t* __restrict__ perm,
-                                                            uint64_t n, const uint32_t* count,
+                                                            uint64_t n, uint32_t* count,
                                                             uint32_t nq_wg, uint32_t pace,
                                                             uint32_t relay_extra, uint32_t slots,
+                                                            uint32_t relay_cap8,
                                                             uint8_t* __restrict__ out) {
+  // beside a relay: count this workgroup in (count[3]) for the relay's gate
+  if (relay_extra && threadIdx.x == 0)
+    __hip_atomic_fetch_add(count + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (lane_paced_wgs(count, nq_wg, pace) != 0) return;
   const uint32_t nl = quad_part_chains(count[0], nq_wg);
   const uint64_t j = nl + (uint64_t)blockIdx.x * kThreads + threadIdx.x;
   // the last relay_extra chains are relayed (k_desc_relay) when it runs
-  const uint64_t end =
-      desc_relay_on(count, nq_wg, len, perm, n, relay_extra, slots) ? n - relay_extra : n;
+  const uint64_t end = desc_relay_on(count, nq_wg, len, perm, n, relay_extra, slots, relay_cap8)
+                           ? n - relay_extra
+                           : n;
   if (j >= end) return;
   const uint32_t b = perm[j];
   uint64_t h[8];
@@ -1474,18 +1481,28 @@ static hipError_t launch_desc_relay(const uint8_t* arena, const uint64_t* off,
                                     const uint32_t* len, const uint32_t* perm, uint64_t n,
                                     uint32_t* n_long, uint32_t nq, uint32_t extra,
                                     uint32_t slots, uint32_t groups, uint32_t nseg_max,
-                                    uint32_t qmin, uint32_t min_seg, const RelayScratch& r,
-                                    uint8_t* out, hipStream_t st) {
+                                    uint32_t qmin, uint32_t min_seg, uint32_t cap8,
+                                    uint32_t gate_target, const RelayScratch& r, uint8_t* out,
+                                    hipStream_t st) {
   uint32_t polls = 0;  // 0: the device's bound; CIR_RELAY_POLLS=0: give up at once
   if (const char* v = getenv("CIR_RELAY_POLLS"))
     polls = std::max(1u, (uint32_t)strtoul(v, nullptr, 10));
+  if (gate_target) {
+    // the relay's waves go in after the lane workgroups hold their CUs
+    // (count[3], bounded wait), so they take the room the lane part's
+    // padding leaves instead of taking the SIMDs first
+    hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, st, n_long + 3, gate_target, 600u);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(k_desc_relay, dim3(groups * nseg_max), dim3(64), 0, st, arena, off, len,
                      perm, n, n_long, nq, extra, slots, groups, nseg_max, polls, qmin, min_seg,
-                     r.flags, r.state, out);
+                     cap8, r.flags, r.state, out);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_desc_relay_finish, dim3(groups), dim3(64), 0, st, arena, off, len, perm, n,
-                     n_long, nq, extra, slots, nseg_max, qmin, min_seg, r.flags, r.state, out);
+                     n_long, nq, extra, slots, nseg_max, qmin, min_seg, cap8, r.flags, r.state,
+                     out);
   return hipGetLastError();
 }
 
@@ -1497,6 +1514,8 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
   // a relay of the chains past k whole lane waves per SIMD (desc_relay_on
   // decides on the device whether it runs)
   const uint64_t slots = 64ull * device_simds();
+  // the most a lane-regime relay takes, in eighths of a lane wave per SIMD
+  const uint32_t cap8 = (uint32_t)relay_env("CIR_RELAY_DCAP8", 5);
   uint32_t extra = 0, groups = 0, nseg_max = 1;
   if (relay && relay->flags && qs != s && aux != qs && desc_may_relay_slots(n, slots)) {
     extra = (uint32_t)(n % slots);
@@ -1532,8 +1551,10 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
     // the other case at once), and the helper behind the quad part
     if (extra) {
       // on qs behind the quad part (which is empty whenever the relay runs)
+      const uint64_t lane_wgs = std::min<uint64_t>(lane_grid, 2ull * device_simds() / 4ull);
       e = launch_desc_relay(arena, off, len, perm, n, n_long, (uint32_t)nq, extra,
-                            (uint32_t)slots, groups, nseg_max, 0u, kRelayMinSegLines, *relay, out,
+                            (uint32_t)slots, groups, nseg_max, 0u, kRelayMinSegLines, cap8,
+                            relay_env("CIR_RELAY_GATE", 1) ? (uint32_t)lane_wgs : 0u, *relay, out,
                             qs);
       if (e != hipSuccess) return e;
     }
@@ -1542,7 +1563,7 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
     // the lane body is issue-bound, two waves per SIMD run it as fast
     hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads),
                        extra ? kRelayDescLanePad : 0u, aux, arena, off, len, perm, n, n_long,
-                       (uint32_t)nq, pace, extra, (uint32_t)slots, out);
+                       (uint32_t)nq, pace, extra, (uint32_t)slots, cap8, out);
     if (pace != 0) {
       e = hipGetLastError();
       if (e != hipSuccess) return e;
@@ -1570,11 +1591,12 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
           (uint32_t)std::max<uint64_t>(1, relay_target_waves(device_simds()) / qgroups);
       e = launch_desc_relay(arena, off, len, perm, n, n_long, (uint32_t)nq, qextra,
                             (uint32_t)qslots, qgroups, qnseg, qmin,
-                            qk == 1 ? relay_quad1_seg() : kRelayMinSegLines, *relay, out, aux);
+                            qk == 1 ? relay_quad1_seg() : kRelayMinSegLines, 0u, 0u, *relay,
+                            out, aux);
       if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads), 0, aux, arena, off,
-                       len, perm, n, n_long, (uint32_t)nq, 0u, 0u, (uint32_t)slots, out);
+                       len, perm, n, n_long, (uint32_t)nq, 0u, 0u, (uint32_t)slots, 0u, out);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_quad_long<kQuadAsm, false>), dim3((unsigned)nq), dim3(kThreads),
