@@ -1138,7 +1138,7 @@ def desc_batch_check(gpu, ctx, oracle, lens, offs_skew, seed):
     assert first_bad(got, want) is None, "descriptor %s" % first_bad(got, want)
 
 
-@pytest.mark.parametrize("case", ["uniform1", "uniform1000", "ragged", "k2", "k4", "longq",
+@pytest.mark.parametrize("case", ["uniform1", "uniform1000", "ragged", "k2", "k4", "wide", "longq",
                                   "q1", "q2", "q2ragged", "q2short", "qmixed"])
 @pytest.mark.parametrize("polls", [None, "0"])
 def test_desc_relay(gpu, ctx, oracle, case, polls, monkeypatch):
@@ -1168,6 +1168,8 @@ def test_desc_relay(gpu, ctx, oracle, case, polls, monkeypatch):
         lens = [4096] * (2 * slots + 4000)
     elif case == "k4":  # the lane part padded to two waves per SIMD beside the relay
         lens = [8192] * (4 * slots + 1500)
+    elif case == "wide":  # 9/16 of a lane wave per SIMD relayed, behind the gate
+        lens = [32768] * (slots + slots * 9 // 16)
     elif case == "longq":
         lens = [32768] * (slots + 300) + [1 << 18] * 20
         rng.shuffle(lens)
