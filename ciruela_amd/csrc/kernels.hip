@@ -1576,9 +1576,11 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
     }
   } else {
     // small batch: a relay of the chains past k whole quad waves per SIMD
-    // on the lane part's stream (aux; the caller's stream by default) beside
-    // the quad part on qs (desc_qrelay_on decides on the device), whose
-    // workgroups are then padded to one per CU to leave room for it
+    // (desc_qrelay_on decides on the device).  Every relay runs on qs (they
+    // share the device's relay scratch, so one stream orders them), so the
+    // quad part then runs on the lane part's stream (aux; the caller's by
+    // default) after the lane part, which is empty whenever the relay runs,
+    // padded to one workgroup per CU to leave room for the relay's waves.
     const uint64_t qslots = 16ull * device_simds();
     uint32_t qextra = 0, qmin = 0;
     if (relay && relay->flags && relay_enabled() && aux != qs && n >= qslots &&
@@ -1592,7 +1594,7 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
       e = launch_desc_relay(arena, off, len, perm, n, n_long, (uint32_t)nq, qextra,
                             (uint32_t)qslots, qgroups, qnseg, qmin,
                             qk == 1 ? relay_quad1_seg() : kRelayMinSegLines, 0u, 0u, *relay,
-                            out, aux);
+                            out, qs);
       if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads), 0, aux, arena, off,
@@ -1600,8 +1602,8 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_quad_long<kQuadAsm, false>), dim3((unsigned)nq), dim3(kThreads),
-                       qextra ? kRelayQuadPad : 0u, qs, arena, off, len, perm, n_long,
-                       (uint32_t)nq, out, n, qextra, qmin);
+                       qextra ? kRelayQuadPad : 0u, qextra ? aux : qs, arena, off, len, perm,
+                       n_long, (uint32_t)nq, out, n, qextra, qmin);
   }
   e = hipGetLastError();
   if (e == hipSuccess && qs != s) e = hipEventRecord(qjoin, qs);

@@ -55,9 +55,10 @@ hipError_t launch_uniform(Loader loader, const uint8_t* data, uint64_t bs, uint6
 hipError_t launch_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint8_t* out,
                          hipStream_t s);
 
-// Device scratch of the relay (k_quad_relay): a flag and 64 x 16 B of chain
-// values per group of 16 chains (one quad-mode wave).  Used on qs only,
-// so calls on one device's qs need no other ordering.
+// Device scratch of the relays (k_quad_relay, k_desc_relay): a flag and
+// 64 x 16 B of chain values per group of 16 chains (one quad-mode wave).
+// Every relay runs on the device's quad-part stream (qs), so relays of
+// different calls are ordered by that one stream.
 struct RelayScratch {
   uint32_t* flags = nullptr;
   uint64_t* state = nullptr;

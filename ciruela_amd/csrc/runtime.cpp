@@ -185,17 +185,22 @@ static hipError_t create_part_streams(Device& d) {
 }
 
 // The relay scratch (kernels.hpp RelayScratch), allocated at full capacity
-// on first use: chain values, then the flags, zeroed once on the quad-part
-// stream (each relay's finisher zeroes its groups' flags again).  Caller
-// holds d.order_mu with d's device current and the part streams created.
+// on first use: chain values, then the flags, zeroed once (each relay's
+// finisher zeroes its groups' flags again).  Every relay runs on the
+// quad-part stream, so relays of different callers never overlap on it.
+// Caller holds d.order_mu with d's device current and the part streams
+// created.
 int ensure_relay(Device& d) {
   if (d.relay_mem) return CIR_OK;
   CIR_HIP(hipMalloc(&d.relay_mem, dev::relay_scratch_bytes(dev::kRelayMaxGroups)));
   d.relay.state = (uint64_t*)d.relay_mem;
   d.relay.flags = (uint32_t*)((uint8_t*)d.relay_mem + (size_t)dev::kRelayMaxGroups * 1024u);
   d.relay.groups = dev::kRelayMaxGroups;
+  // zeroed before any relay can run (once per device; the relays themselves
+  // all run on the quad-part stream, in order)
   CIR_HIP(hipMemsetAsync(d.relay.flags, 0, (size_t)dev::kRelayMaxGroups * 4u,
                          d.qstream ? d.qstream : d.compute));
+  CIR_HIP(hipStreamSynchronize(d.qstream ? d.qstream : d.compute));
   return CIR_OK;
 }
 
