@@ -1187,3 +1187,60 @@ def test_desc_relay(gpu, ctx, oracle, case, polls, monkeypatch):
         lens = [32768] * (2 * qslots + 100) + [rng.randrange(0, 1000) for _ in range(10)]
         rng.shuffle(lens)
     desc_batch_check(gpu, ctx, oracle, lens, skew, seed=len(lens))
+
+
+def test_relays_from_concurrent_callers(gpu, ctx, oracle):
+    """A chunk-form relay and both descriptor relays (lane and quad regime)
+    issued from three threads on three streams of one context at once: the
+    relays share the device's scratch and are ordered by its quad-part
+    stream; every digest against the oracle."""
+    import threading
+    import torch
+    slots = lane_wave_slots()
+    jobs = []
+    # chunk form: one lane wave per SIMD + 3 blocks of 32 KiB
+    nb1 = slots + 3
+    d1 = dev_random(gpu, nb1 * 32768, seed=71)
+    o1 = torch.zeros(nb1 * 32, dtype=torch.uint8, device="cuda:0")
+    jobs.append(("chunks", d1, o1, nb1 * 32768))
+    # descriptor batches: lane regime (slots + 5 x 16 KiB), quad regime
+    # (slots / 4 + 7 x 64 KiB)
+    for name, n, bs, seed in (("desc_lane", slots + 5, 16384, 72), ("desc_quad", slots // 4 + 7, 65536, 73)):
+        d = dev_random(gpu, n * bs, seed=seed)
+        off = torch.arange(n, dtype=torch.int64, device="cuda:0") * bs
+        ln = torch.full((n,), bs, dtype=torch.int32, device="cuda:0")
+        o = torch.zeros(n * 32, dtype=torch.uint8, device="cuda:0")
+        jobs.append((name, d, o, (off, ln, n, bs)))
+    streams = [torch.cuda.Stream() for _ in jobs]
+    torch.cuda.synchronize()
+    errors = []
+
+    def run(job, st):
+        try:
+            name, d, o, arg = job
+            for _ in range(3):
+                if name == "chunks":
+                    ctx.hash_chunks_dev(d.data_ptr(), arg, 32768, o.data_ptr(), st.cuda_stream)
+                else:
+                    off, ln, n, _ = arg
+                    ctx.hash_blocks_dev(d.data_ptr(), off.data_ptr(), ln.data_ptr(), n,
+                                        o.data_ptr(), st.cuda_stream)
+            st.synchronize()
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+
+    th = [threading.Thread(target=run, args=(j, st)) for j, st in zip(jobs, streams)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
+    for name, d, o, arg in jobs:
+        host = d.cpu().numpy()
+        if name == "chunks":
+            want = oracle_chunks(oracle, host, arg, 32768)
+        else:
+            _, _, n, bs = arg
+            want = oracle_chunks(oracle, host, n * bs, bs)
+        got = o.cpu().numpy()
+        assert first_bad(got, want) is None, (name, first_bad(got, want))
