@@ -462,6 +462,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))
 // flags[g] = segments of group g done (zeroed before the launch).
 // ---------------------------------------------------------------------------
 constexpr uint32_t kRelayGroupChains = 16;
+#ifndef CIR_RELAY_LIGHT
+#define CIR_RELAY_LIGHT 1
+#endif
 #ifndef CIR_RELAY_SLEEP
 #define CIR_RELAY_SLEEP 8  // s_sleep units (64 clocks): ~0.25 us between polls
 #endif
@@ -597,7 +600,7 @@ __device__ __forceinline__ void relay_segment(const R& r, uint32_t g, uint32_t s
       if (k >= max_polls) return;  // the finisher takes over from here
       __builtin_amdgcn_s_sleep(CIR_RELAY_SLEEP);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (!CIR_RELAY_LIGHT) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __builtin_amdgcn_s_setprio(3);
   uint64_t h0, h1;
@@ -606,9 +609,16 @@ __device__ __forceinline__ void relay_segment(const R& r, uint32_t g, uint32_t s
     if (s == 0) {
       quad_init(lane & 3u, h0, h1);
     } else {
-      const uint64_t* st = state + ((uint64_t)g * 64u + lane) * 2u;
-      h0 = st[0];
-      h1 = st[1];
+      uint64_t* st = state + ((uint64_t)g * 64u + lane) * 2u;
+      if (CIR_RELAY_LIGHT) {
+        // agent-scope loads (sc1): coherent across XCDs without the L2
+        // invalidate of an acquire fence; issued after the flag was seen
+        h0 = __hip_atomic_load(st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        h1 = __hip_atomic_load(st + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        h0 = st[0];
+        h1 = st[1];
+      }
     }
   }
   if (nu) {
@@ -640,13 +650,25 @@ __device__ __forceinline__ void relay_segment(const R& r, uint32_t g, uint32_t s
       *reinterpret_cast<uint64_t*>(out + r.block(c) * 32u + 8u * (lane & 3u)) = h0;
     } else {
       uint64_t* st = state + ((uint64_t)g * 64u + lane) * 2u;
-      st[0] = h0;
-      st[1] = h1;
+      if (CIR_RELAY_LIGHT) {
+        __hip_atomic_store(st, h0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(st + 1, h1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        st[0] = h0;
+        st[1] = h1;
+      }
     }
   }
   if (!publish) return;
-  // the chain values (or digests) reach every XCD's view before the flag
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  // the chain values reach every XCD's view before the flag: agent-scope
+  // stores (sc1, written through to the coherent level) completed by
+  // vmcnt(0) -- no L2 write-back of a release fence; the digests are read
+  // only after the kernel (CIR_RELAY_LIGHT=0: the fences of round 2's first
+  // relay)
+  if (CIR_RELAY_LIGHT)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   if (lane == 0)
     __hip_atomic_store(flags + g, group_final ? 0xffffffffu : s + 1u, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
