@@ -716,10 +716,10 @@ __device__ __forceinline__ uint32_t quad_part_chains(uint32_t n_long, uint32_t n
 
 // Relay of a small descriptor batch (quad regime, launch_mixed): the host
 // launches one when n = 16384 k + extra (16 chains per quad wave, one wave
-// per SIMD per k), extra <= 1/4 of that; it runs only when every chain of
+// per SIMD per k), extra <= 1/2 of that; it runs only when every chain of
 // the batch is in the quad part (count[0] == n, so the split is exact) and
 // the longest relayed chain has >= min_lines lines (the chunk-form rule:
-// 64 at k = 1, 32 above).
+// 64 at k = 1, 32 above, 128 past 1/4 of a wave).
 __device__ __forceinline__ bool desc_qrelay_on(const uint32_t* count, const uint32_t* len,
                                                const uint32_t* perm, uint64_t n, uint32_t extra,
                                                uint32_t min_lines) {
@@ -1286,6 +1286,18 @@ static uint64_t relay_env(const char* name, uint64_t dflt) {
   return e ? strtoull(e, nullptr, 10) : dflt;
 }
 
+// Quad regime: extra chains of up to 1/2 of a quad wave per SIMD relay
+// (CIR_RELAY_QFRAC / CIR_RELAY_DQFRAC = d: up to 1/d, chunk form /
+// descriptors); past 1/4 only chains of >= 128 lines (32 KiB x 24576
+// 1283 -> 1535 GiB/s, 1 MiB x 24576 1301 -> 1690; 3/4 is no better than
+// none: profiles/r02/relay/qfrac/).
+static bool quad_relay_fits(uint64_t extra, uint64_t qslots, bool desc) {
+  return extra * relay_env(desc ? "CIR_RELAY_DQFRAC" : "CIR_RELAY_QFRAC", 2) <= qslots;
+}
+static uint32_t quad_relay_min_lines(uint64_t k, uint64_t extra, uint64_t qslots) {
+  return extra * 4 > qslots ? 128u : (k == 1 ? 64u : 32u);
+}
+
 static uint32_t relay_quad1_seg() {  // CIR_RELAY_QSEG1: A/B of the k = 1 quad segments
   static const uint32_t v = [] {
     const char* e = getenv("CIR_RELAY_QSEG1");
@@ -1321,9 +1333,10 @@ struct RelayPlan {
 // wave per SIMD (lines/512 below 64 lines); beyond that one more lane wave (or the quad band of
 // chunks_in_quad) costs less than the relayed chains' quad-mode work
 // (profiles/r02/relay/).  Quad regime (below one lane wave per SIMD):
-// k >= 1 whole quad waves per SIMD plus up to 1/4 of one (1/64 past the
-// small-batch limit), chains of >= 64 lines at k = 1 (>= 32 above: shorter
-// relays cost more than they save).  16 <= lines, bs < 2^31.
+// k >= 1 whole quad waves per SIMD plus up to 1/2 of one (1/64 past the
+// small-batch limit), chains of >= 64 lines at k = 1 (>= 32 above, >= 128
+// past 1/4 of a wave: shorter relays cost more than they save).
+// 16 <= lines, bs < 2^31.
 static bool relay_plan(uint64_t nfull, uint64_t bs, RelayPlan& p) {
   p = RelayPlan();
   if (!relay_enabled() || bs % 128u != 0 || bs < 128u * 16u || bs >= (1ull << 31)) return false;
@@ -1341,8 +1354,8 @@ static bool relay_plan(uint64_t nfull, uint64_t bs, RelayPlan& p) {
     // (profiles/r02/relay/qshort/); past the small-batch limit (k = 3)
     // lane mode takes over from 1/64 of a quad wave of extra blocks on
     const uint64_t k = nfull / quad_slots, extra = nfull % quad_slots;
-    if (lines < relay_env("CIR_RELAY_QLINES", k == 1 ? 64 : 32) || k < relay_min_quad_k() ||
-        extra == 0 || extra * 4 > quad_slots ||
+    if (extra == 0 || k < relay_min_quad_k() || !quad_relay_fits(extra, quad_slots, false) ||
+        lines < relay_env("CIR_RELAY_QLINES", quad_relay_min_lines(k, extra, quad_slots)) ||
         (nfull >= quad_small_batch() && extra * 64 > quad_slots))
       return false;
     p.base = nfull - extra;
@@ -1374,7 +1387,7 @@ static bool desc_may_relay_slots(uint64_t n, uint64_t slots) {
 bool desc_may_relay(uint64_t n) {
   const uint64_t qslots = 16ull * device_simds();
   const bool quad_regime = relay_enabled() && n < quad_small_batch() && n >= qslots &&
-                           n % qslots != 0 && (n % qslots) * 4 <= qslots;
+                           n % qslots != 0 && quad_relay_fits(n % qslots, qslots, true);
   return quad_regime || desc_may_relay_slots(n, 64ull * device_simds());
 }
 
@@ -1606,11 +1619,11 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
     const uint64_t qslots = 16ull * device_simds();
     uint32_t qextra = 0, qmin = 0;
     if (relay && relay->flags && relay_enabled() && aux != qs && n >= qslots &&
-        n % qslots != 0 && (n % qslots) * 4 <= qslots) {
+        n % qslots != 0 && quad_relay_fits(n % qslots, qslots, true)) {
       qextra = (uint32_t)(n % qslots);
       const uint32_t qgroups = (qextra + kRelayGroupChains - 1) / kRelayGroupChains;
       const uint32_t qk = (uint32_t)(n / qslots);
-      qmin = qk == 1 ? 64u : 32u;
+      qmin = quad_relay_min_lines(qk, qextra, qslots);
       const uint32_t qnseg =
           (uint32_t)std::max<uint64_t>(1, relay_target_waves(device_simds()) / qgroups);
       e = launch_desc_relay(arena, off, len, perm, n, n_long, (uint32_t)nq, qextra,

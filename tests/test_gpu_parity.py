@@ -1041,11 +1041,14 @@ RELAY_SHAPES = [
     (65536, "1q", 2, 0),       # 1 quad wave per SIMD + 2 chains
     (32768, "3q", 4, 0),       # past the small-batch limit: quad base of 3 waves
     (4096, "2q", 77, 3),       # 32-line chains beside 2 quad waves per SIMD
+    (16384, "1q", "q/2", 5),   # half a quad wave per SIMD of 128-line chains
 ]
 
 
 def relay_nfull(k, extra):
     slots = lane_wave_slots()
+    if extra == "q/2":
+        extra = slots // 8
     if isinstance(k, str):
         return int(k[:-1]) * slots // 4 + extra
     return k * slots + extra
@@ -1062,6 +1065,8 @@ def test_chunks_dev_relay(gpu, ctx, oracle, bs, k, extra, tail, polls, monkeypat
     if polls is not None:
         monkeypatch.setenv("CIR_RELAY_POLLS", polls)
     nfull = relay_nfull(k, extra)
+    if extra == "q/2":
+        extra = lane_wave_slots() // 8
     assert gpu._n.lib.cir_debug_relay_blocks(nfull, bs) == extra
     nbytes = nfull * bs + tail
     data = dev_random(gpu, nbytes, seed=nfull ^ bs)
@@ -1078,9 +1083,10 @@ def test_chunks_dev_relay(gpu, ctx, oracle, bs, k, extra, tail, polls, monkeypat
 def test_relay_rule_bounds(gpu):
     """No relay below one quad wave per SIMD, beyond k = 16 lane waves, past
     5/8 of a lane wave (lines / 256 for short chains, lines / 512 below 64
-    lines) or 1/4 of a quad wave
+    lines) or 1/2 of a quad wave
     (1/64 past the small-batch limit) of extra blocks, below 16 lines, or in
-    the quad regime below 128 lines."""
+    the quad regime below 64 lines at k = 1 / 32 above (128 past 1/4 of a
+    quad wave)."""
     slots = lane_wave_slots()
     qslots = slots // 4
     f = gpu._n.lib.cir_debug_relay_blocks
@@ -1105,7 +1111,10 @@ def test_relay_rule_bounds(gpu):
     assert f(2 * qslots + 1, 2048) == 0
     assert f(2 * qslots + 1, 32768) == 1
     assert f(2 * qslots + qslots // 4, 32768) == qslots // 4
-    assert f(2 * qslots + qslots // 4 + 1, 32768) == 0
+    assert f(2 * qslots + qslots // 4 + 1, 8192) == 0
+    assert f(2 * qslots + qslots // 4 + 1, 16384) == qslots // 4 + 1
+    assert f(qslots + qslots // 2, 16384) == qslots // 2
+    assert f(2 * qslots + qslots // 2 + 1, 32768) == 0
     assert f(3 * qslots + qslots // 64, 32768) == qslots // 64
     assert f(3 * qslots + qslots // 64 + 1, 32768) == 0
 
@@ -1139,7 +1148,7 @@ def desc_batch_check(gpu, ctx, oracle, lens, offs_skew, seed):
 
 
 @pytest.mark.parametrize("case", ["uniform1", "uniform1000", "ragged", "k2", "k4", "wide", "longq",
-                                  "q1", "q2", "q2ragged", "q2short", "qmixed"])
+                                  "q1", "q2", "q2ragged", "q2short", "qhalf", "qmixed"])
 @pytest.mark.parametrize("polls", [None, "0"])
 def test_desc_relay(gpu, ctx, oracle, case, polls, monkeypatch):
     """Descriptor batches of k lane waves per SIMD plus a few chains: the
@@ -1183,6 +1192,9 @@ def test_desc_relay(gpu, ctx, oracle, case, polls, monkeypatch):
         skew = lambda i: 3 if i % 17 == 0 else 0  # noqa: E731
     elif case == "q2short":
         lens = [4096] * (2 * qslots + 999)
+    elif case == "qhalf":  # half a quad wave per SIMD relayed, ragged at the end
+        lens = [16384] * (qslots + qslots // 2 - 40) + [rng.randrange(1, 16384) for _ in range(40)]
+        rng.shuffle(lens)
     else:
         lens = [32768] * (2 * qslots + 100) + [rng.randrange(0, 1000) for _ in range(10)]
         rng.shuffle(lens)
