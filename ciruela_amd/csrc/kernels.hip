@@ -1566,8 +1566,21 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
   if (lane_grid > 0x7fffffffull) return hipErrorInvalidValue;
   const uint32_t pace = aux != qs ? lane_pace() : 0u;  // only beside a concurrent quad part
   const bool exclusive = CIR_QUAD_EXCLUSIVE && n >= quad_small_batch();
+  // small batch: a relay of the chains past k whole quad waves per SIMD
+  // (desc_qrelay_on decides on the device)
+  const uint64_t qslots = 16ull * device_simds();
+  uint32_t qextra = 0;
+  if (!exclusive && relay && relay->flags && relay_enabled() && aux != qs && n >= qslots &&
+      n % qslots != 0 && quad_relay_fits(n % qslots, qslots, true))
+    qextra = (uint32_t)(n % qslots);
+  // Small batches run both parts on aux, one after the other (the lane part
+  // holds only chains of < 8 lines): qs only carries a relay, and without
+  // one the fork to qs and the join back cost ~25 us of a 0.4 ms batch
+  // (32 KiB x 16384, profiles/r02/desc/serial/)
+  const bool serial = !exclusive && n < quad_small_batch() && qextra == 0;
+  const bool qs_used = qs != s && !serial;
   hipError_t e = hipEventRecord(fork, s);
-  if (e == hipSuccess && qs != s) e = hipStreamWaitEvent(qs, fork, 0);
+  if (e == hipSuccess && qs_used) e = hipStreamWaitEvent(qs, fork, 0);
   if (e == hipSuccess && aux != s) e = hipStreamWaitEvent(aux, fork, 0);
   if (e != hipSuccess) return e;
   if (exclusive) {
@@ -1610,17 +1623,13 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
                          off, len, perm, n, n_long, (uint32_t)nq, pace, 1u, out);
     }
   } else {
-    // small batch: a relay of the chains past k whole quad waves per SIMD
-    // (desc_qrelay_on decides on the device).  Every relay runs on qs (they
-    // share the device's relay scratch, so one stream orders them), so the
-    // quad part then runs on the lane part's stream (aux; the caller's by
-    // default) after the lane part, which is empty whenever the relay runs,
-    // padded to one workgroup per CU to leave room for the relay's waves.
-    const uint64_t qslots = 16ull * device_simds();
-    uint32_t qextra = 0, qmin = 0;
-    if (relay && relay->flags && relay_enabled() && aux != qs && n >= qslots &&
-        n % qslots != 0 && quad_relay_fits(n % qslots, qslots, true)) {
-      qextra = (uint32_t)(n % qslots);
+    // Every relay runs on qs (they share the device's relay scratch, so one
+    // stream orders them); the quad part runs on the lane part's stream (aux;
+    // the caller's by default) after the lane part, which is empty whenever
+    // the relay runs, padded to one workgroup per CU beside a relay to leave
+    // room for the relay's waves.
+    uint32_t qmin = 0;
+    if (qextra) {
       const uint32_t qgroups = (qextra + kRelayGroupChains - 1) / kRelayGroupChains;
       const uint32_t qk = (uint32_t)(n / qslots);
       qmin = quad_relay_min_lines(qk, qextra, qslots);
@@ -1637,13 +1646,13 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_quad_long<kQuadAsm, false>), dim3((unsigned)nq), dim3(kThreads),
-                       qextra ? kRelayQuadPad : 0u, qextra ? aux : qs, arena, off, len, perm,
-                       n_long, (uint32_t)nq, out, n, qextra, qmin);
+                       qextra ? kRelayQuadPad : 0u, qs_used && !qextra ? qs : aux, arena, off,
+                       len, perm, n_long, (uint32_t)nq, out, n, qextra, qmin);
   }
   e = hipGetLastError();
-  if (e == hipSuccess && qs != s) e = hipEventRecord(qjoin, qs);
+  if (e == hipSuccess && qs_used) e = hipEventRecord(qjoin, qs);
   if (e == hipSuccess && aux != s) e = hipEventRecord(ljoin, aux);
-  if (e == hipSuccess && qs != s) e = hipStreamWaitEvent(s, qjoin, 0);
+  if (e == hipSuccess && qs_used) e = hipStreamWaitEvent(s, qjoin, 0);
   if (e == hipSuccess && aux != s) e = hipStreamWaitEvent(s, ljoin, 0);
   return e;
 }
