@@ -529,12 +529,14 @@ struct RelayDesc {
 };
 
 // Extra blocks a relay takes at most, as lines / relay_cap_div(lines) of a
-// lane wave per SIMD: at 32-line chains a relay of 1/8 of a wave was no
-// faster than one more lane wave (4 KiB x 73728 / 139264 blocks), so short
-// chains get half the allowance.
-__host__ __device__ __forceinline__ uint64_t relay_cap_div(uint64_t lines) {
-  return lines < 64 ? 512 : 256;
-}
+// lane wave per SIMD (and at most 5/8 of one): 1/4 of a wave of 16-line
+// chains, 1/2 of 32-line ones, 5/8 from 40 lines on.  With the prefetching
+// lane part and the fence-free hand-off this pays at every measured short
+// shape (4 KiB x 73728 1403-1424 -> 1675-1700 GiB/s, x 147456 1475-1492 ->
+// 1779-1847, 8 KiB x 98304 1581-1603 -> 1793-1832, 2 KiB x 139264
+// 1431-1439 -> 1718-1725; profiles/r02/relay/capdiv/), where lines / 512
+// (below 64 lines) and lines / 256 had not before.
+__host__ __device__ __forceinline__ uint64_t relay_cap_div(uint64_t) { return 64; }
 
 // Compressions of a chain of L bytes (the empty input compresses once).
 __device__ __forceinline__ uint32_t chain_lines(uint64_t L) {
@@ -1329,8 +1331,8 @@ struct RelayPlan {
 };
 
 // Lane regime (nfull >= one lane wave per SIMD): k = 1 .. CIR_RELAY_MAXK whole
-// lane waves per SIMD plus extra blocks up to min(5/8, lines/256) of a lane
-// wave per SIMD (lines/512 below 64 lines); beyond that one more lane wave (or the quad band of
+// lane waves per SIMD plus extra blocks up to min(5/8, lines/64) of a lane
+// wave per SIMD (relay_cap_div); beyond that one more lane wave (or the quad band of
 // chunks_in_quad) costs less than the relayed chains' quad-mode work
 // (profiles/r02/relay/).  Quad regime (below one lane wave per SIMD):
 // k >= 1 whole quad waves per SIMD plus up to 1/2 of one (1/64 past the
@@ -1344,7 +1346,8 @@ static bool relay_plan(uint64_t nfull, uint64_t bs, RelayPlan& p) {
   const uint64_t lane_slots = 64ull * simds, quad_slots = 16ull * simds;
   if (nfull >= lane_slots) {
     const uint64_t k = nfull / lane_slots, extra = nfull % lane_slots;
-    const uint64_t cap = std::min(lane_slots * 5 / 8, lane_slots * lines / relay_cap_div(lines));
+    const uint64_t cap = std::min(
+        lane_slots * 5 / 8, lane_slots * lines / relay_env("CIR_RELAY_CAPDIV", relay_cap_div(lines)));
     if (k > relay_max_k() || extra == 0 || extra > cap) return false;
     p.base = nfull - extra;
     p.nrel = extra;

@@ -1042,13 +1042,17 @@ RELAY_SHAPES = [
     (32768, "3q", 4, 0),       # past the small-batch limit: quad base of 3 waves
     (4096, "2q", 77, 3),       # 32-line chains beside 2 quad waves per SIMD
     (16384, "1q", "q/2", 5),   # half a quad wave per SIMD of 128-line chains
+    (4096, 1, "l/2", 0),       # half a lane wave per SIMD of 32-line chains
 ]
+
+
+def relay_extra(extra):
+    return {"q/2": lane_wave_slots() // 8, "l/2": lane_wave_slots() // 2}.get(extra, extra)
 
 
 def relay_nfull(k, extra):
     slots = lane_wave_slots()
-    if extra == "q/2":
-        extra = slots // 8
+    extra = relay_extra(extra)
     if isinstance(k, str):
         return int(k[:-1]) * slots // 4 + extra
     return k * slots + extra
@@ -1065,8 +1069,7 @@ def test_chunks_dev_relay(gpu, ctx, oracle, bs, k, extra, tail, polls, monkeypat
     if polls is not None:
         monkeypatch.setenv("CIR_RELAY_POLLS", polls)
     nfull = relay_nfull(k, extra)
-    if extra == "q/2":
-        extra = lane_wave_slots() // 8
+    extra = relay_extra(extra)
     assert gpu._n.lib.cir_debug_relay_blocks(nfull, bs) == extra
     nbytes = nfull * bs + tail
     data = dev_random(gpu, nbytes, seed=nfull ^ bs)
@@ -1082,8 +1085,7 @@ def test_chunks_dev_relay(gpu, ctx, oracle, bs, k, extra, tail, polls, monkeypat
 
 def test_relay_rule_bounds(gpu):
     """No relay below one quad wave per SIMD, beyond k = 16 lane waves, past
-    5/8 of a lane wave (lines / 256 for short chains, lines / 512 below 64
-    lines) or 1/2 of a quad wave
+    min(5/8, lines / 64) of a lane wave or 1/2 of a quad wave
     (1/64 past the small-batch limit) of extra blocks, below 16 lines, or in
     the quad regime below 64 lines at k = 1 / 32 above (128 past 1/4 of a
     quad wave)."""
@@ -1098,8 +1100,11 @@ def test_relay_rule_bounds(gpu):
     assert f(17 * slots + 1, 32768) == 0
     assert f(slots + slots * 5 // 8, 32768) == slots * 5 // 8
     assert f(slots + slots * 5 // 8 + 1, 32768) == 0
-    assert f(slots + slots // 16, 4096) == slots // 16
-    assert f(slots + slots // 16 + 1, 4096) == 0
+    assert f(slots + slots // 2, 4096) == slots // 2
+    assert f(slots + slots // 2 + 1, 4096) == 0
+    assert f(slots + slots // 4, 2048) == slots // 4
+    assert f(slots + slots // 4 + 1, 2048) == 0
+    assert f(slots + slots * 5 // 8, 8192) == slots * 5 // 8
     assert f(slots + slots // 4, 8192) == slots // 4
     assert f(slots + 1, 1024) == 0
     assert f(slots + 1, 2048) == 1
@@ -1148,7 +1153,8 @@ def desc_batch_check(gpu, ctx, oracle, lens, offs_skew, seed):
 
 
 @pytest.mark.parametrize("case", ["uniform1", "uniform1000", "ragged", "k2", "k4", "wide", "longq",
-                                  "q1", "q2", "q2ragged", "q2short", "qhalf", "qmixed"])
+                                  "q1", "q2", "q2ragged", "q2short", "qhalf", "qmixed",
+                                  "shorthalf"])
 @pytest.mark.parametrize("polls", [None, "0"])
 def test_desc_relay(gpu, ctx, oracle, case, polls, monkeypatch):
     """Descriptor batches of k lane waves per SIMD plus a few chains: the
@@ -1192,6 +1198,8 @@ def test_desc_relay(gpu, ctx, oracle, case, polls, monkeypatch):
         skew = lambda i: 3 if i % 17 == 0 else 0  # noqa: E731
     elif case == "q2short":
         lens = [4096] * (2 * qslots + 999)
+    elif case == "shorthalf":  # half a lane wave per SIMD of 32-line chains
+        lens = [4096] * (slots + slots // 2)
     elif case == "qhalf":  # half a quad wave per SIMD relayed, ragged at the end
         lens = [16384] * (qslots + qslots // 2 - 40) + [rng.randrange(1, 16384) for _ in range(40)]
         rng.shuffle(lens)
