@@ -529,14 +529,15 @@ struct RelayDesc {
 };
 
 // Extra blocks a relay takes at most, as lines / relay_cap_div(lines) of a
-// lane wave per SIMD (and at most 5/8 of one): 1/4 of a wave of 16-line
-// chains, 1/2 of 32-line ones, 5/8 from 40 lines on.  With the prefetching
-// lane part and the fence-free hand-off this pays at every measured short
-// shape (4 KiB x 73728 1403-1424 -> 1675-1700 GiB/s, x 147456 1475-1492 ->
-// 1779-1847, 8 KiB x 98304 1581-1603 -> 1793-1832, 2 KiB x 139264
-// 1431-1439 -> 1718-1725; profiles/r02/relay/capdiv/), where lines / 512
-// (below 64 lines) and lines / 256 had not before.
-__host__ __device__ __forceinline__ uint64_t relay_cap_div(uint64_t) { return 64; }
+// lane wave per SIMD (and at most 5/8 of one): 1/2 of a wave of 16-line
+// chains, 5/8 from 20 lines on.  With the prefetching lane part and the
+// fence-free hand-off this pays at every measured short shape (4 KiB x
+// 73728 1403-1424 -> 1675-1700 GiB/s, x 106496 1337-1407 -> 1515-1562,
+// 8 KiB x 98304 1581-1603 -> 1793-1832, 2 KiB x 139264 1431-1439 ->
+// 1718-1725; 16-line chains past 1/4 of a wave neither gain nor lose;
+// profiles/r02/relay/capdiv/), where lines / 512 (below 64 lines) and
+// lines / 256 had not before.
+__host__ __device__ __forceinline__ uint64_t relay_cap_div(uint64_t) { return 32; }
 
 // Compressions of a chain of L bytes (the empty input compresses once).
 __device__ __forceinline__ uint32_t chain_lines(uint64_t L) {
@@ -1331,7 +1332,7 @@ struct RelayPlan {
 };
 
 // Lane regime (nfull >= one lane wave per SIMD): k = 1 .. CIR_RELAY_MAXK whole
-// lane waves per SIMD plus extra blocks up to min(5/8, lines/64) of a lane
+// lane waves per SIMD plus extra blocks up to min(5/8, lines/32) of a lane
 // wave per SIMD (relay_cap_div); beyond that one more lane wave (or the quad band of
 // chunks_in_quad) costs less than the relayed chains' quad-mode work
 // (profiles/r02/relay/).  Quad regime (below one lane wave per SIMD):

@@ -1085,7 +1085,7 @@ def test_chunks_dev_relay(gpu, ctx, oracle, bs, k, extra, tail, polls, monkeypat
 
 def test_relay_rule_bounds(gpu):
     """No relay below one quad wave per SIMD, beyond k = 16 lane waves, past
-    min(5/8, lines / 64) of a lane wave or 1/2 of a quad wave
+    min(5/8, lines / 32) of a lane wave or 1/2 of a quad wave
     (1/64 past the small-batch limit) of extra blocks, below 16 lines, or in
     the quad regime below 64 lines at k = 1 / 32 above (128 past 1/4 of a
     quad wave)."""
@@ -1100,10 +1100,10 @@ def test_relay_rule_bounds(gpu):
     assert f(17 * slots + 1, 32768) == 0
     assert f(slots + slots * 5 // 8, 32768) == slots * 5 // 8
     assert f(slots + slots * 5 // 8 + 1, 32768) == 0
-    assert f(slots + slots // 2, 4096) == slots // 2
-    assert f(slots + slots // 2 + 1, 4096) == 0
-    assert f(slots + slots // 4, 2048) == slots // 4
-    assert f(slots + slots // 4 + 1, 2048) == 0
+    assert f(slots + slots * 5 // 8, 4096) == slots * 5 // 8
+    assert f(slots + slots * 5 // 8 + 1, 4096) == 0
+    assert f(slots + slots // 2, 2048) == slots // 2
+    assert f(slots + slots // 2 + 1, 2048) == 0
     assert f(slots + slots * 5 // 8, 8192) == slots * 5 // 8
     assert f(slots + slots // 4, 8192) == slots // 4
     assert f(slots + 1, 1024) == 0
