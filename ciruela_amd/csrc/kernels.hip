@@ -1347,8 +1347,9 @@ static bool relay_plan(uint64_t nfull, uint64_t bs, RelayPlan& p) {
   const uint64_t lane_slots = 64ull * simds, quad_slots = 16ull * simds;
   if (nfull >= lane_slots) {
     const uint64_t k = nfull / lane_slots, extra = nfull % lane_slots;
-    const uint64_t cap = std::min(
-        lane_slots * 5 / 8, lane_slots * lines / relay_env("CIR_RELAY_CAPDIV", relay_cap_div(lines)));
+    const uint64_t cap =
+        std::min(lane_slots * relay_env("CIR_RELAY_CAP8", 5) / 8,
+                 lane_slots * lines / relay_env("CIR_RELAY_CAPDIV", relay_cap_div(lines)));
     if (k > relay_max_k() || extra == 0 || extra > cap) return false;
     p.base = nfull - extra;
     p.nrel = extra;
