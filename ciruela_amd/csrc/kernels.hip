@@ -1243,8 +1243,11 @@ hipError_t launch_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint
 // Falls back to launch_chunks where the split does not apply.
 // CIR_RELAY=0 turns the relay off (A/B); CIR_RELAY_SEGS = the segment waves
 // one relay aims at (default: one per SIMD).
+// Relays run up to 32 whole lane waves per SIMD (17 - 20 measured: 32 KiB x
+// 1114113 blocks 2066-2070 -> 2193 GiB/s, x 1310721 2094-2099 -> 2193-2203,
+// as descriptors +3-5 %; profiles/r02/relay/maxk/).
 #ifndef CIR_RELAY_MAXK
-#define CIR_RELAY_MAXK 16
+#define CIR_RELAY_MAXK 32
 #endif
 // With k >= 3 lane waves per SIMD the lane part is launched with
 // kRelayLanePad bytes of extra LDS per workgroup: two k_chunks workgroups

@@ -79,7 +79,7 @@ hipError_t launch_chunks_split(const uint8_t* data, uint64_t nbytes, uint64_t bs
 // of nfull whole blocks of bs bytes on the current device.
 uint64_t relay_blocks(uint64_t nfull, uint64_t bs);
 // Whether launch_mixed may relay the last chains of a descriptor batch of n
-// chains on the current device (1 .. 16 lane waves per SIMD and a few more,
+// chains on the current device (1 .. 32 lane waves per SIMD and a few more,
 // or a small batch of whole quad waves per SIMD and a few more).
 bool desc_may_relay(uint64_t n);
 

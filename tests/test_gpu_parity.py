@@ -1043,6 +1043,7 @@ RELAY_SHAPES = [
     (4096, "2q", 77, 3),       # 32-line chains beside 2 quad waves per SIMD
     (16384, "1q", "q/2", 5),   # half a quad wave per SIMD of 128-line chains
     (4096, 1, "l/2", 0),       # half a lane wave per SIMD of 32-line chains
+    (2048, 17, 5, 0),          # past 16 lane waves per SIMD
 ]
 
 
@@ -1084,7 +1085,7 @@ def test_chunks_dev_relay(gpu, ctx, oracle, bs, k, extra, tail, polls, monkeypat
 
 
 def test_relay_rule_bounds(gpu):
-    """No relay below one quad wave per SIMD, beyond k = 16 lane waves, past
+    """No relay below one quad wave per SIMD, beyond k = 32 lane waves, past
     min(5/8, lines / 32) of a lane wave or 1/2 of a quad wave
     (1/64 past the small-batch limit) of extra blocks, below 16 lines, or in
     the quad regime below 64 lines at k = 1 / 32 above (128 past 1/4 of a
@@ -1097,7 +1098,9 @@ def test_relay_rule_bounds(gpu):
     assert f(slots + 1, 32768) == 1
     assert f(3 * slots + 1, 32768) == 1
     assert f(16 * slots + 5, 32768) == 5
-    assert f(17 * slots + 1, 32768) == 0
+    assert f(17 * slots + 1, 32768) == 1
+    assert f(32 * slots + 7, 32768) == 7
+    assert f(33 * slots + 1, 32768) == 0
     assert f(slots + slots * 5 // 8, 32768) == slots * 5 // 8
     assert f(slots + slots * 5 // 8 + 1, 32768) == 0
     assert f(slots + slots * 5 // 8, 4096) == slots * 5 // 8
