@@ -20,8 +20,11 @@ bounded sample of the same config-2 blocks, at 4 threads (the reference's
 default --disk-threads) and at all host cores (<= 16).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--loader glds|direct]
-    python bench.py --workload config3|config5|config1   (secondary configs,
-        reported in DESIGN.md; not the headline line)
+    python bench.py --workload config3|config5|config1|config2host|config2sha
+        (one secondary config on its own; the default N=1 line also carries
+        config3 and config2host as `secondary` records)
+    python bench.py --gpus N   (N > 1: launches N ranks itself through
+        torch.distributed.run unless WORLD_SIZE is already set)
 """
 import argparse
 import ctypes
@@ -62,9 +65,14 @@ def parse():
                    help="staging buffer size of the host paths (0 = library default, 256)")
     p.add_argument("--tree-dir", default="/dev/shm/ciruela_bench_tree")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-secondary", action="store_true",
+                   help="N=1 default line without the secondary config3 / config2host records")
     p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                    help="process group of the N>1 path (nccl = RCCL; gloo for rehearsals "
                         "with several ranks per GPU)")
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher and process-group plumbing only (gloo, no GPU, no hashing): "
+                        "prints the line skeleton with the ranks the job saw (CPU tests)")
     p.add_argument("--force-dist", action="store_true",
                    help="run the N>1 code path (process group, config 4) even at world size 1")
     p.add_argument("--cpu-seconds", type=float, default=2.5,
@@ -109,8 +117,10 @@ def load_oracle():
 
 # CPU share of one GPU on the measurement boxes: gpurun gives a one-GPU box
 # 16 host CPUs (OMP_NUM_THREADS / MAX_JOBS are set to 16 there) while
-# os.cpu_count() and the affinity mask show the whole host.  "All cores" of
-# the CPU baseline is therefore min(affinity, 16); host_info() records both.
+# os.cpu_count() and the affinity mask show the whole host.  The CPU baseline
+# therefore has three legs over the same sample: 4 threads (the reference's
+# default --disk-threads, src/client/global_options.rs:13), the per-GPU share
+# (min(affinity, 16) threads) and every CPU in the affinity mask.
 CPU_SHARE_PER_GPU = 16
 
 
@@ -128,16 +138,21 @@ def host_info():
             "cpu_model": model, "cpu_share_per_gpu": CPU_SHARE_PER_GPU}
 
 
-def all_cores():
+def per_gpu_share():
     return max(1, min(CPU_SHARE_PER_GPU, len(os.sched_getaffinity(0))))
+
+
+def all_affinity():
+    return max(1, len(os.sched_getaffinity(0)))
 
 
 def cpu_rates(run, target_s):
     """run(threads) -> bytes hashed by one pass over the sample; repeated
     until `target_s` wall seconds at 4 threads (the same CPU work, so
-    target_s * 4 / threads, at more threads).  {threads: (GiB/s, bytes)}."""
+    target_s * 4 / threads, at more threads; at least one pass).
+    {threads: (GiB/s, bytes)} for 4, the per-GPU share and all affinity CPUs."""
     res = {}
-    for threads in sorted({4, all_cores()}):
+    for threads in sorted({4, per_gpu_share(), all_affinity()}):
         wall = target_s * 4.0 / threads if threads > 4 else target_s
         done, t0 = 0, time.perf_counter()
         while True:
@@ -150,11 +165,15 @@ def cpu_rates(run, target_s):
 
 
 def cpu_record(res, sample, unit="GiB/s"):
-    t4, ac = res[4], res[all_cores()]
+    t4, pg, aa = res[4], res[per_gpu_share()], res[all_affinity()]
     return {"value": round(t4[0], 4), "unit": unit, "cores": 4, "kind": "port",
             "sample": sample,
-            "all_cores": {"value": round(ac[0], 4), "cores": all_cores(),
-                          "sample_bytes": ac[1]},
+            "per_gpu_share": {"value": round(pg[0], 4), "cores": per_gpu_share(),
+                              "sample_bytes": pg[1],
+                              "note": "the host CPUs one GPU's job gets on the measurement box"},
+            "all_affinity": {"value": round(aa[0], 4), "cores": all_affinity(),
+                             "sample_bytes": aa[1],
+                             "note": "one thread per CPU of the process affinity mask"},
             "host": host_info()}
 
 
@@ -294,12 +313,22 @@ def run_config3(args, ca, ctx, dev, stream):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    # HIP events around each batch's ordering, quad part and lane part on the
+    # streams they run on, recorded by the library over the timed steps
+    lib = ca._n.lib
+    ca._n.check(lib.cir_debug_desc_timing(ctx.handle, 1))
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
+    parts = (ctypes.c_double * 5)()
+    ca._n.check(lib.cir_debug_desc_times(ctx.handle, parts))
+    ca._n.check(lib.cir_debug_desc_timing(ctx.handle, 0))
+    nb = max(1.0, parts[0])
+    order_ms, quad_ms, lane_ms, total_ms = (parts[k] / nb for k in (1, 2, 3, 4))
     hashed = int(lens.astype("int64").sum())
+    algo = hashed + 32 * n
     got = out.cpu().numpy().reshape(-1, 32)
     del data, out
     torch.cuda.empty_cache()
@@ -307,7 +336,7 @@ def run_config3(args, ca, ctx, dev, stream):
     # oracle check + CPU baseline on the same sample: the first descriptors
     # whose blocks fill the first 2 GiB of the arena (shuffled order, so all
     # three classes and the ragged lengths are in it), regenerated on the host
-    lib = load_oracle()
+    lib = load_oracle()  # noqa: F811 (the oracle from here on)
     k = int(np.searchsorted(offs, 2 << 30))
     prefix = int(offs[k - 1] + (lens[k - 1] + 127) // 128 * 128)
     host = np.empty(prefix // 8, dtype=np.uint64)
@@ -329,6 +358,19 @@ def run_config3(args, ca, ctx, dev, stream):
             "config": {"workload": "config3: 10 GiB of 4 KiB / 32 KiB / 1 MiB blocks (equal bytes "
                                    "per class), 10 % ragged, shuffled, device-resident"},
             "matches_oracle": matches, "oracle_checked_blocks": k,
+            "roofline": {
+                "bound": "hbm", "achieved": round(algo / (total_ms / 1e3) / 1e9, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(algo / (total_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                "traffic": None, "kernel": "k_quad_long (dominant; 1 MiB chains in quad mode)",
+                "kernel_ms_avg": round(quad_ms, 4), "batch_kernel_ms_avg": round(total_ms, 4),
+                "parts_ms_avg": {"ordering": round(order_ms, 4), "quad_part": round(quad_ms, 4),
+                                 "lane_part": round(lane_ms, 4)},
+                "timed_batches": int(parts[0]),
+                "note": "achieved = (sum of lengths + 32 B per digest) / (ordering start -> "
+                        "last part end), HIP events on the streams the kernels run on; the "
+                        "quad part is latency-bound (8192 dependent compressions per 1 MiB "
+                        "chain), not HBM-bound: see DESIGN.md 4.2"},
             "cpu_baseline": cpu_record(rates, "the first %d descriptors of the config-3 order "
                                        "(%.2f GiB, all classes, ragged included), "
                                        "oracle_hash_blocks; 4 threads = reference default "
@@ -466,7 +508,10 @@ def make_tree(root, gib, file_mib=32, ndirs=40, seed=0x5EED0005):
     return nfiles
 
 
-def run_config5(args, ca, ctx):
+def run_config5(args, ca, ctx, ctx_init_s=None):
+    """value = best of the scans; value_first = the first scan of this
+    process, which is what one `ciruela sync` sees (it scans once per run,
+    src/client/sync/mod.rs:192-201)."""
     t0 = time.perf_counter()
     nfiles = make_tree(args.tree_dir, args.tree_gib)
     gen_s = time.perf_counter() - t0
@@ -490,7 +535,7 @@ def run_config5(args, ca, ctx):
     import cpu_indexer
     lib = cpu_indexer.load()
     t0 = time.perf_counter()
-    want = cpu_indexer.index(args.tree_dir, 32768, all_cores(), lib)
+    want = cpu_indexer.index(args.tree_dir, 32768, per_gpu_share(), lib)
     full_s = time.perf_counter() - t0
     # 4 threads (the reference default) on a bounded sample: directories
     # d00..d03 (a tenth of the files), indexed as their own trees
@@ -507,11 +552,14 @@ def run_config5(args, ca, ctx):
                      "oracle/cpu_indexer.py (file-level pool, block_size reads, C BLAKE2b); "
                      "4 threads = reference default --disk-threads" % (
                          sum(len(os.listdir(d)) for d in sample), sample_bytes / GIB))
-    cpu["full_tree"] = {"seconds": round(full_s, 3), "cores": all_cores(),
+    cpu["full_tree"] = {"seconds": round(full_s, 3), "cores": per_gpu_share(),
                         "value": round(nbytes / full_s / GIB, 4)}
     return {"metric": "GiB/s end-to-end index of a tmpfs tree (config 5)",
             "value": round(nbytes / best / GIB, 3), "unit": "GiB/s",
             "seconds_best": round(best, 3), "seconds_all": [round(t, 3) for t in times],
+            "seconds_first": round(times[0], 3),
+            "value_first": round(nbytes / times[0] / GIB, 3),
+            "context_init_s": round(ctx_init_s, 3) if ctx_init_s is not None else None,
             "config": {"workload": "config5: %d files x 32 MiB in 40 dirs (%.0f GiB) on tmpfs, "
                                    "cir_scan_v1 (reads -> pinned -> H2D -> hash -> D2H, footer "
                                    "on the GPU)" % (nfiles, nbytes / GIB)},
@@ -575,21 +623,113 @@ def run_config1(args, ca, ctx):
                     "`ciruela-index sync` process including HIP start-up"}
 
 
+def run_secondary(args, ca, ctx, dev, stream):
+    """The secondary BASELINE configs carried in the default N=1 line, so the
+    driver's own run observes them: config 3 (mixed 4K/32K/1M descriptors,
+    device-resident) and config 2 from host memory (the PCIe-inclusive rate).
+    Each is a record of its own (value, roofline or seconds, cpu_baseline,
+    matches_oracle); a failure is recorded, not raised."""
+    import copy
+    import traceback
+    out = {}
+    legs = (("config3", run_config3, dict(steps=min(args.steps, 10), warmup=min(args.warmup, 2))),
+            ("config2host", run_config2host, dict(steps=min(args.steps, 3))))
+    for name, fn, over in legs:
+        a = copy.copy(args)
+        for k, v in over.items():
+            setattr(a, k, v)
+        t0 = time.perf_counter()
+        try:
+            out[name] = fn(a, ca, ctx, dev, stream)
+        except Exception as e:  # noqa: BLE001 - reported in the line
+            traceback.print_exc()
+            out[name] = {"error": "%s: %s" % (type(e).__name__, e), "matches_oracle": False}
+        out[name]["wall_s"] = round(time.perf_counter() - t0, 1)
+        import torch
+        torch.cuda.empty_cache()
+    return out
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(nproc, argv):
+    """`bench.py --gpus N` (N > 1) without a launcher around it: start N rank
+    processes through torch.distributed.run (one per GPU, rendezvous on
+    127.0.0.1) as children of this process, which has touched no GPU, and
+    exit with their status.  Rank 0 writes the one JSON line to the stdout
+    this process shares with it."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(nproc), "--master-addr", "127.0.0.1",
+           "--master-port", str(free_port()), os.path.abspath(__file__)] + list(argv)
+    log("bench: launching %d ranks: %s" % (nproc, " ".join(cmd)))
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    sys.stdout.flush()
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args, rank, world):
+    """The N>1 line's plumbing without a GPU: process group (gloo), shard
+    plan, timed region and max-over-ranks, one JSON line from rank 0."""
+    import torch
+    import torch.distributed as dist
+    distributed = world > 1 or args.force_dist
+    if distributed:
+        dist.init_process_group("gloo")
+    first, count = shard(rank, world, args.blocks)
+    elapsed = timed_steps(lambda i: time.sleep(0.01), args.steps, lambda: None,
+                          dist.barrier if distributed else None)
+    elapsed_max = max_over_ranks(elapsed)
+    bounds = torch.tensor([first, count], dtype=torch.int64)
+    parts = [torch.zeros_like(bounds) for _ in range(world)]
+    if distributed:
+        dist.all_gather(parts, bounds)
+    else:
+        parts = [bounds]
+    if rank == 0:
+        print(json.dumps({
+            "dry_run": True, "metric": METRIC, "n_gpus": world,
+            "ranks_seen": dist.get_world_size() if distributed else 1,
+            "steps": args.steps, "ms_per_step": round(elapsed_max / max(1, args.steps) * 1e3, 4),
+            "config": {"workload": "config4" if distributed else "config2",
+                       "blocks_per_gpu": args.blocks, "block_size": args.block_size},
+            "shards": [p.tolist() for p in parts]}), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+    return 0
+
+
 def main():
     args = parse()
+    # --gpus N > 1 with no launcher: spawn the ranks before anything touches a
+    # GPU (no torch.cuda call has run in this process yet; never exec)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args.gpus, sys.argv[1:])
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         log("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+    if args.dry_run:
+        return dry_run(args, rank, world)
     import torch
     import torch.distributed as dist
 
     import ciruela_amd as ca
 
-    # one rank per GPU; more ranks than GPUs (a rehearsal of the N>1 path on a
-    # small box, gloo only: RCCL refuses two ranks on one GPU) share them
+    # one rank per GPU; more ranks than GPUs only as a rehearsal of the N>1
+    # path on a small box with gloo (RCCL refuses two ranks on one GPU)
     ndev = max(1, torch.cuda.device_count())
+    if world > ndev and args.dist_backend == "nccl":
+        raise SystemExit("bench: %d ranks but %d visible GPU(s): one rank per GPU over RCCL; "
+                         "use --dist-backend gloo for a rehearsal with shared GPUs"
+                         % (world, ndev))
     ranks_per_gpu = (world + ndev - 1) // ndev if world > ndev else 1
     if ranks_per_gpu > 1:
         log("warning: %d ranks on %d GPU(s): ranks share GPUs (rehearsal, not a scaling run)"
@@ -619,13 +759,15 @@ def main():
     nblk = args.blocks
     nbytes = nblk * bs
     stream = torch.cuda.current_stream().cuda_stream
+    t0 = time.perf_counter()
     ctx = ca.Context(device_mask=1 << (local % ndev), staging_bytes=args.staging_mib << 20)
+    ctx_init_s = time.perf_counter() - t0
 
     if args.workload != "auto":
         if world != 1:
             raise SystemExit("secondary workloads run on one GPU")
         rec = {"config3": lambda: run_config3(args, ca, ctx, dev, stream),
-               "config5": lambda: run_config5(args, ca, ctx),
+               "config5": lambda: run_config5(args, ca, ctx, ctx_init_s),
                "config1": lambda: run_config1(args, ca, ctx),
                "config2host": lambda: run_config2host(args, ca, ctx, dev, stream),
                "config2sha": lambda: run_config2sha(args, ca, ctx, dev, stream)}[args.workload]()
@@ -739,12 +881,23 @@ def main():
             },
             "parity": parity,
         }
+        if distributed:
+            # the process group's own count: every rank of the job took part
+            rec["ranks_seen"] = dist.get_world_size()
+            rec["dist_backend"] = args.dist_backend
         if c4_checked:
             rec["parity_checked_blocks"] = c4_checked
         if ranks_per_gpu > 1:
             rec["config"]["ranks_per_gpu"] = ranks_per_gpu
         if not distributed and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(bs, args.cpu_seconds)
+        if not distributed and not args.no_secondary:
+            del data, out, ref_out
+            torch.cuda.empty_cache()
+            rec["secondary"] = run_secondary(args, ca, ctx, dev, stream)
+            if any(not r.get("matches_oracle", False) for r in rec["secondary"].values()):
+                parity = "FAIL: a secondary config differs from the oracle"
+                rec["parity"] = parity
         print(json.dumps(rec), flush=True)
     if distributed:
         dist.destroy_process_group()

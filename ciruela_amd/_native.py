@@ -103,6 +103,8 @@ _SIGS = {
                                       ctypes.c_size_t, ctypes.POINTER(ctypes.c_int)]),
     "cir_debug_compress_only_dev": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, c_vp, c_vp]),
     "cir_debug_relay_blocks": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint64]),
+    "cir_debug_desc_timing": (ctypes.c_int, [c_vp, ctypes.c_int]),
+    "cir_debug_desc_times": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double)]),
     "cir_debug_hash_uniform_dev": (ctypes.c_int, [ctypes.c_int, c_vp, ctypes.c_uint64,
                                                   ctypes.c_uint64, c_vp, c_vp]),
     "cir_fill_splitmix64_dev": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint64,

@@ -346,6 +346,12 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
   return __builtin_amdgcn_readfirstlane(v);
 }
 
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int s = 1; s < 64; s <<= 1) v = max(v, (uint32_t)__shfl_xor((int)v, s));
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
 // Lines of a quad's chain that quad_fast may take: full, not final, from a
 // 16-B aligned start (0 for an inactive quad of the wave: it does not run).
 #ifndef CIR_QUAD_FAST
@@ -504,10 +510,13 @@ __device__ __forceinline__ uint32_t lane_now() {
 }
 
 // The chains a relay hands on, c = 0 .. n-1: the blocks b0 + c of a file
-// of bs-byte blocks (chunk form, every chain the same length) or the chains
-// first + c of an ordered descriptor batch (sorted longest first, so the
-// first chain of a group of 16 is its longest).
+// of bs-byte blocks (chunk form, every chain the same length: kUniform) or
+// the chains first + c of an ordered descriptor batch.  The order is by
+// length bin (order.hip), exact only below 2048 lines: above that one bin
+// spans several lengths in arbitrary order, so a group's first chain need not
+// be its longest and relay_segment takes the group's maximum.
 struct RelayFile {
+  static constexpr bool kUniform = true;
   const uint8_t* data;
   uint64_t bs, b0;
   uint32_t n;
@@ -517,6 +526,7 @@ struct RelayFile {
 };
 
 struct RelayDesc {
+  static constexpr bool kUniform = false;
   const uint8_t* arena;
   const uint64_t* off;
   const uint32_t* len;
@@ -560,10 +570,19 @@ __device__ __forceinline__ void relay_segment(const R& r, uint32_t g, uint32_t s
                                               uint64_t* state, uint8_t* __restrict__ out,
                                               uint8_t* lds, uint32_t max_polls, bool publish) {
   const uint32_t l0 = s * seg_lines;
-  const uint32_t group_lines = chain_lines(r.bytes(g * kRelayGroupChains));
+  auto chain = [&](uint32_t lane) { return g * kRelayGroupChains + (lane >> 2); };
+  // the group's longest chain decides whether this segment has work and
+  // whether it finishes the group (the final flag): every chain of the group,
+  // not only its first, must have ended when the flag says so
+  uint32_t group_lines;
+  if constexpr (R::kUniform) {
+    group_lines = chain_lines(r.bytes(0));
+  } else {
+    const uint32_t c = chain(lane_now());
+    group_lines = wave_max_u32(c < r.n ? chain_lines(r.bytes(c)) : 0u);
+  }
   if (l0 >= group_lines && s > 0) return;
   const bool group_final = l1_max >= group_lines;
-  auto chain = [&](uint32_t lane) { return g * kRelayGroupChains + (lane >> 2); };
   // lines of this lane's chain in the segment; nu = the wave's common run
   // of full, not final, 16-B aligned lines for the hand-scheduled loop
   uint32_t nu = 0;
@@ -1392,13 +1411,6 @@ static bool desc_may_relay_slots(uint64_t n, uint64_t slots) {
          (n % slots + kRelayGroupChains - 1) / kRelayGroupChains <= kRelayMaxGroups;
 }
 
-bool desc_may_relay(uint64_t n) {
-  const uint64_t qslots = 16ull * device_simds();
-  const bool quad_regime = relay_enabled() && n < quad_small_batch() && n >= qslots &&
-                           n % qslots != 0 && quad_relay_fits(n % qslots, qslots, true);
-  return quad_regime || desc_may_relay_slots(n, 64ull * device_simds());
-}
-
 // Blocks [b0, b0 + nrel) of a file of whole bs-byte blocks as relayed quad
 // chains on qs (the relay, then its finisher, which zeroes the flags
 // again).  Segments of at least kRelayMinSegLines lines, as many as make
@@ -1552,8 +1564,14 @@ static hipError_t launch_desc_relay(const uint8_t* arena, const uint64_t* off,
 hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
                         const uint32_t* perm, uint32_t* n_long, uint64_t n, uint8_t* out,
                         hipStream_t s, hipStream_t qs, hipStream_t aux, hipEvent_t fork,
-                        hipEvent_t qjoin, hipEvent_t ljoin, const RelayScratch* relay) {
+                        hipEvent_t qjoin, hipEvent_t ljoin, const RelayScratch* relay,
+                        const hipEvent_t* tev) {
   if (n == 0) return hipSuccess;
+  // tev (diagnostics): quad part start / end on its stream, lane part start /
+  // end on aux (the lane part's kernels after the gate)
+  auto mark = [&](int k, hipStream_t st) {
+    return tev ? hipEventRecord(tev[k], st) : hipSuccess;
+  };
   // a relay of the chains past k whole lane waves per SIMD (desc_relay_on
   // decides on the device whether it runs)
   const uint64_t slots = 64ull * device_simds();
@@ -1578,7 +1596,10 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
   // (desc_qrelay_on decides on the device)
   const uint64_t qslots = 16ull * device_simds();
   uint32_t qextra = 0;
-  if (!exclusive && relay && relay->flags && relay_enabled() && aux != qs && n >= qslots &&
+  // (a relay runs only on the device's own quad-part stream, never on the
+  // caller's: relays share the device's scratch, one stream orders them)
+  if (!exclusive && relay && relay->flags && relay_enabled() && qs != s && aux != qs &&
+      n >= qslots &&
       n % qslots != 0 && quad_relay_fits(n % qslots, qslots, true))
     qextra = (uint32_t)(n % qslots);
   // Small batches run both parts on aux, one after the other (the lane part
@@ -1596,9 +1617,12 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
     // they are dispatched first, and the lane part starts once all of them
     // hold their CUs (k_gate), so its waves fill the other CUs instead of
     // taking every SIMD first.
+    e = mark(0, qs);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_quad_long<kQuadAsm, true>), dim3((unsigned)nq), dim3(kThreads), 0, qs,
                        arena, off, len, perm, n_long, (uint32_t)nq, out, n, 0u, 0u);
     e = hipGetLastError();
+    if (e == hipSuccess) e = mark(1, qs);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, aux, n_long + 1, (uint32_t)nq, 600u);
     e = hipGetLastError();
@@ -1617,6 +1641,8 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
     // beside a relay at most two lane waves per SIMD (2 x 128 VGPRs, two
     // 64 KiB-padded workgroups per CU), so a relay wave (244) always fits;
     // the lane body is issue-bound, two waves per SIMD run it as fast
+    e = mark(2, aux);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads),
                        extra ? kRelayDescLanePad : 0u, aux, arena, off, len, perm, n, n_long,
                        (uint32_t)nq, pace, extra, (uint32_t)slots, cap8, out);
@@ -1626,9 +1652,14 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
       hipLaunchKernelGGL(k_lane_tiles, dim3((unsigned)lane_grid), dim3(kThreads), 0, aux, arena,
                          off, len, perm, n, n_long, (uint32_t)nq, pace, 0u, out);
       e = hipGetLastError();
+      if (e == hipSuccess) e = mark(3, aux);
       if (e != hipSuccess) return e;
       hipLaunchKernelGGL(k_lane_tiles, dim3((unsigned)lane_grid), dim3(kThreads), 0, qs, arena,
                          off, len, perm, n, n_long, (uint32_t)nq, pace, 1u, out);
+    } else {
+      e = hipGetLastError();
+      if (e == hipSuccess) e = mark(3, aux);
+      if (e != hipSuccess) return e;
     }
   } else {
     // Every relay runs on qs (they share the device's relay scratch, so one
@@ -1649,13 +1680,22 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
                             out, qs);
       if (e != hipSuccess) return e;
     }
+    e = mark(2, aux);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads), 0, aux, arena, off,
                        len, perm, n, n_long, (uint32_t)nq, 0u, 0u, (uint32_t)slots, 0u, out);
     e = hipGetLastError();
+    if (e == hipSuccess) e = mark(3, aux);
+    if (e != hipSuccess) return e;
+    hipStream_t qst = qs_used && !qextra ? qs : aux;
+    e = mark(0, qst);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_quad_long<kQuadAsm, false>), dim3((unsigned)nq), dim3(kThreads),
-                       qextra ? kRelayQuadPad : 0u, qs_used && !qextra ? qs : aux, arena, off,
-                       len, perm, n_long, (uint32_t)nq, out, n, qextra, qmin);
+                       qextra ? kRelayQuadPad : 0u, qst, arena, off, len, perm, n_long,
+                       (uint32_t)nq, out, n, qextra, qmin);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = mark(1, qst);
+    if (e != hipSuccess) return e;
   }
   e = hipGetLastError();
   if (e == hipSuccess && qs_used) e = hipEventRecord(qjoin, qs);

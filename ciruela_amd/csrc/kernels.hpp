@@ -78,10 +78,6 @@ hipError_t launch_chunks_split(const uint8_t* data, uint64_t nbytes, uint64_t bs
 // Number of blocks launch_chunks_split would relay (0: no relay) for a file
 // of nfull whole blocks of bs bytes on the current device.
 uint64_t relay_blocks(uint64_t nfull, uint64_t bs);
-// Whether launch_mixed may relay the last chains of a descriptor batch of n
-// chains on the current device (1 .. 32 lane waves per SIMD and a few more,
-// or a small batch of whole quad waves per SIMD and a few more).
-bool desc_may_relay(uint64_t n);
 
 // Blocks first .. first+n-1 of Hashes::hash_file's split of [data, data+nbytes).
 hipError_t launch_general_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs,
@@ -98,11 +94,14 @@ hipError_t launch_general_desc(const uint8_t* arena, const uint64_t* off, const 
 // join back into s (`qjoin`, `ljoin`).
 // relay (nullable): scratch for relaying the chains past k whole lane (or
 // quad) waves per SIMD (k_desc_relay; decided on the device).
+// tev (nullable, diagnostics): 4 timing events recorded around the quad
+// part (0, 1; on its stream) and the lane part (2, 3; on aux).
 hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
                         const uint32_t* perm, uint32_t* n_long, uint64_t n, uint8_t* out,
                         hipStream_t s, hipStream_t qs, hipStream_t aux, hipEvent_t fork,
                         hipEvent_t qjoin, hipEvent_t ljoin,
-                        const RelayScratch* relay = nullptr);
+                        const RelayScratch* relay = nullptr,
+                        const hipEvent_t* tev = nullptr);
 
 // Longest-chain-first order of a descriptor batch (order.hip): *perm points
 // into `scratch` (order_scratch_bytes(n) bytes, device memory).

@@ -54,6 +54,9 @@ Device::~Device() {
   }
   (void)hipFree(chain_state);
   if (chain) (void)hipStreamDestroy(chain);
+  for (auto& set : tev)
+    for (hipEvent_t e : set)
+      if (e) (void)hipEventDestroy(e);
   if (order_free) (void)hipEventSynchronize(order_free);
   (void)hipFree(order_scratch);
   if (order_free) (void)hipEventDestroy(order_free);
@@ -185,12 +188,12 @@ static hipError_t create_part_streams(Device& d) {
 }
 
 // The relay scratch (kernels.hpp RelayScratch), allocated at full capacity
-// on first use: chain values, then the flags, zeroed once (each relay's
+// by cir_init: chain values, then the flags, zeroed once (each relay's
 // finisher zeroes its groups' flags again).  Every relay runs on the
 // quad-part stream, so relays of different callers never overlap on it.
 // Caller holds d.order_mu with d's device current and the part streams
 // created.
-int ensure_relay(Device& d) {
+static int ensure_relay(Device& d) {
   if (d.relay_mem) return CIR_OK;
   CIR_HIP(hipMalloc(&d.relay_mem, dev::relay_scratch_bytes(dev::kRelayMaxGroups)));
   d.relay.state = (uint64_t*)d.relay_mem;
@@ -204,9 +207,9 @@ int ensure_relay(Device& d) {
   return CIR_OK;
 }
 
-// The part streams and their events, created on first use (caller holds
+// The part streams and their events, created by cir_init (caller holds
 // d.order_mu with d's device current).
-int ensure_part_streams(Device& d) {
+static int ensure_part_streams(Device& d) {
   if (d.order_free) return CIR_OK;
   CIR_HIP(create_part_streams(d));
   CIR_HIP(hipEventCreateWithFlags(&d.aux_fork, hipEventDisableTiming));
@@ -243,8 +246,8 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
   DeviceGuard guard;
   CIR_HIP(hipSetDevice(d.id));
   const size_t need = dev::order_scratch_bytes(n);
-  int rc = ensure_part_streams(d);
-  if (rc) return rc;
+  // the ordering scratch grows with the batch (the one allocation left on
+  // this path: a batch larger than any before waits for the previous user)
   if (need > d.order_cap) {
     CIR_HIP(hipEventSynchronize(d.order_free));
     (void)hipFree(d.order_scratch);
@@ -253,22 +256,30 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
     CIR_HIP(hipMalloc(&d.order_scratch, need));
     d.order_cap = need;
   }
-  // a batch of at least one lane wave per SIMD may relay its last chains
-  // (launch_mixed); the SIMD count is the device's
-  if (ht != CIR_HASH_SHA512_256 && d.qstream && dev::desc_may_relay(n)) {
-    rc = ensure_relay(d);
-    if (rc) return rc;
-  }
   CIR_HIP(hipStreamWaitEvent(s, d.order_free, 0));
+  // diagnostics: a fresh event set per batch while timing is on (at most
+  // kMaxTimedBatches per enable)
+  constexpr size_t kMaxTimedBatches = 256;
+  const hipEvent_t* tev = nullptr;
+  if (d.timing && ht != CIR_HASH_SHA512_256 && d.tev_used < kMaxTimedBatches) {
+    if (d.tev_used == d.tev.size()) {
+      std::array<hipEvent_t, 6> set{};
+      for (hipEvent_t& e : set) CIR_HIP(hipEventCreate(&e));
+      d.tev.push_back(set);
+    }
+    tev = d.tev[d.tev_used++].data();
+    CIR_HIP(hipEventRecord(tev[0], s));
+  }
   uint32_t* perm = nullptr;
   uint32_t* n_long = nullptr;
   CIR_HIP(dev::launch_order_desc(len, n, d.order_scratch, d.order_cap, &perm, &n_long, s));
+  if (tev) CIR_HIP(hipEventRecord(tev[1], s));
   if (ht == CIR_HASH_SHA512_256)
     CIR_HIP(dev::launch_sha_desc(arena, off, len, perm, n, out, s));
   else
     CIR_HIP(dev::launch_mixed(arena, off, len, perm, n_long, n, out, s, d.qstream ? d.qstream : s,
                               d.aux ? d.aux : s, d.aux_fork, d.q_join, d.aux_join,
-                              d.relay_mem ? &d.relay : nullptr));
+                              d.relay_mem ? &d.relay : nullptr, tev ? tev + 2 : nullptr));
   CIR_HIP(hipEventRecord(d.order_free, s));
   return CIR_OK;
 }
@@ -576,6 +587,20 @@ static int export_hashes(const std::vector<uint8_t>& h, uint8_t** out, size_t* n
   return CIR_OK;
 }
 
+// Everything a device state needs that does not depend on a call's sizes,
+// created here so the asynchronous *_dev entry points never allocate or
+// synchronise: the staging and part streams, their events and the relay
+// scratch (zeroed with one synchronised memset).  Caller holds a DeviceGuard.
+static int init_device(Device& d) {
+  CIR_HIP(hipSetDevice(d.id));
+  CIR_HIP(hipStreamCreateWithFlags(&d.compute, hipStreamNonBlocking));
+  CIR_HIP(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
+  std::lock_guard<std::mutex> lk(d.order_mu);
+  int rc = ensure_part_streams(d);
+  if (rc == CIR_OK) rc = ensure_relay(d);
+  return rc;
+}
+
 // Process-default context for cir_blake2b256 (BlockHash::hash_bytes has no
 // context argument in the reference).
 static std::once_flag g_default_once;
@@ -621,9 +646,8 @@ int cir_init(cir_ctx** out, uint32_t device_mask, uint64_t staging_bytes) {
     if (rc) return rc;
     auto d = std::make_unique<Device>();
     d->id = i;
-    CIR_HIP(hipSetDevice(i));
-    CIR_HIP(hipStreamCreateWithFlags(&d->compute, hipStreamNonBlocking));
-    CIR_HIP(hipStreamCreateWithFlags(&d->copy, hipStreamNonBlocking));
+    rc = init_device(*d);
+    if (rc) return rc;
     ctx->devs.push_back(std::move(d));
   }
   if (ctx->devs.empty()) return fail(CIR_ENODEV, "device_mask selects no visible device");
@@ -637,9 +661,8 @@ int cir_init(cir_ctx** out, uint32_t device_mask, uint64_t staging_bytes) {
       for (size_t i = 0; i < n0; ++i) {
         auto d = std::make_unique<Device>();
         d->id = ctx->devs[i]->id;
-        CIR_HIP(hipSetDevice(d->id));
-        CIR_HIP(hipStreamCreateWithFlags(&d->compute, hipStreamNonBlocking));
-        CIR_HIP(hipStreamCreateWithFlags(&d->copy, hipStreamNonBlocking));
+        const int rc = init_device(*d);
+        if (rc) return rc;
         ctx->devs.push_back(std::move(d));
       }
   }
@@ -687,15 +710,11 @@ int cir_hash_chunks_dev(cir_ctx* ctx, const void* d_data, uint64_t nbytes, uint6
   // device's quad-part stream beside the uniform part (launch_chunks_split)
   Device* d = ctx ? stream_device(ctx, s) : nullptr;
   if (d && nbytes) {
+    // (the part streams and the relay scratch exist since cir_init: nothing
+    // here allocates or synchronises)
     std::lock_guard<std::mutex> lk(d->order_mu);
     DeviceGuard guard;
     CIR_HIP(hipSetDevice(d->id));
-    int rc = ensure_part_streams(*d);
-    if (rc) return rc;
-    if (dev::relay_blocks(nbytes / block_size, block_size) > 0) {
-      rc = ensure_relay(*d);
-      if (rc) return rc;
-    }
     CIR_HIP(dev::launch_chunks_split((const uint8_t*)d_data, nbytes, block_size, d_out, s,
                                      d->qstream, d->aux_fork, d->q_join, &d->relay));
     return CIR_OK;
@@ -780,10 +799,11 @@ static int single_launch(Device& d, const uint8_t* p, size_t n, uint8_t* out) {
   std::lock_guard<std::mutex> lk(d.single_mu);
   DeviceGuard guard;
   CIR_HIP(hipSetDevice(d.id));
-  if (!d.single) {
-    CIR_HIP(hipStreamCreateWithFlags(&d.single, hipStreamNonBlocking));
+  // each resource is checked on its own, so a failure part-way leaves the
+  // rest to be created by the next call (never a launch with a null output)
+  if (!d.single) CIR_HIP(hipStreamCreateWithFlags(&d.single, hipStreamNonBlocking));
+  if (!d.single_out)
     CIR_HIP(hipHostMalloc(&d.single_out, 64, hipHostMallocMapped | hipHostMallocCoherent));
-  }
   const size_t need = (n + 15) & ~(size_t)15;
   if (need > d.single_cap) {
     (void)hipHostFree(d.single_h);
@@ -793,7 +813,12 @@ static int single_launch(Device& d, const uint8_t* p, size_t n, uint8_t* out) {
     d.single_cap = 0;
     const size_t cap = std::max<size_t>(need, 64u << 10);
     CIR_HIP(hipHostMalloc(&d.single_h, cap, hipHostMallocMapped | hipHostMallocCoherent));
-    CIR_HIP(hipMalloc(&d.single_d, cap));
+    const hipError_t e = hipMalloc(&d.single_d, cap);
+    if (e != hipSuccess) {
+      (void)hipHostFree(d.single_h);
+      d.single_h = nullptr;
+      return hip_fail(e, "hipMalloc(single_d)");
+    }
     d.single_cap = cap;
   }
   if (n) memcpy(d.single_h, p, n);
@@ -1023,6 +1048,40 @@ int cir_debug_compress_only_dev(uint64_t nlanes, uint32_t lines, uint8_t* d_out,
   if (nlanes % dev::kThreads || lines == 0 || !d_out)
     return fail(CIR_EINVAL, "compress-only kernel needs nlanes % 256 == 0, lines > 0, an output");
   CIR_HIP(dev::launch_compress_only(nlanes, lines, d_out, (hipStream_t)stream));
+  return CIR_OK;
+}
+
+int cir_debug_desc_timing(cir_ctx* ctx, int enable) {
+  if (!ctx || ctx->devs.empty()) return fail(CIR_EINVAL, "null ctx");
+  Device& d = *ctx->devs[0];
+  std::lock_guard<std::mutex> lk(d.order_mu);
+  d.timing = enable != 0;
+  d.tev_used = 0;
+  return CIR_OK;
+}
+
+int cir_debug_desc_times(cir_ctx* ctx, double out[5]) {
+  if (!ctx || ctx->devs.empty() || !out) return fail(CIR_EINVAL, "null pointer");
+  Device& d = *ctx->devs[0];
+  std::lock_guard<std::mutex> lk(d.order_mu);
+  DeviceGuard guard;
+  CIR_HIP(hipSetDevice(d.id));
+  for (int k = 0; k < 5; ++k) out[k] = 0.0;
+  for (size_t b = 0; b < d.tev_used; ++b) {
+    const auto& e = d.tev[b];
+    for (hipEvent_t x : e) CIR_HIP(hipEventSynchronize(x));
+    float order = 0, quad = 0, lane = 0, to_q = 0, to_l = 0;
+    CIR_HIP(hipEventElapsedTime(&order, e[0], e[1]));
+    CIR_HIP(hipEventElapsedTime(&quad, e[2], e[3]));
+    CIR_HIP(hipEventElapsedTime(&lane, e[4], e[5]));
+    CIR_HIP(hipEventElapsedTime(&to_q, e[0], e[3]));
+    CIR_HIP(hipEventElapsedTime(&to_l, e[0], e[5]));
+    out[0] += 1.0;
+    out[1] += order;
+    out[2] += quad;
+    out[3] += lane;
+    out[4] += std::max(to_q, to_l);
+  }
   return CIR_OK;
 }
 

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <array>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -91,8 +92,8 @@ struct Device {
   int part_mode = 0;
   hipStream_t aux = nullptr, qstream = nullptr;
   hipEvent_t aux_fork = nullptr, aux_join = nullptr, q_join = nullptr;
-  // relayed quad chains of cir_hash_chunks_dev (used on qstream only;
-  // allocated at full capacity on first use, under order_mu)
+  // relayed quad chains (used on qstream only; allocated at full capacity
+  // by cir_init)
   dev::RelayScratch relay;
   void* relay_mem = nullptr;
   // incremental footer chain (cir_scan_v1): own stream, state, text buffers
@@ -111,6 +112,12 @@ struct Device {
   uint8_t* single_d = nullptr;
   uint8_t* single_out = nullptr;
   size_t single_cap = 0;
+  // per-part timing of ordered batches (cir_debug_desc_timing): one set of
+  // six events per recorded batch -- ordering start / end on the caller's
+  // stream, quad part start / end, lane part start / end -- under order_mu
+  bool timing = false;
+  std::vector<std::array<hipEvent_t, 6>> tev;
+  size_t tev_used = 0;
   ~Device();
   int ensure_slot(Slot& s, uint64_t bytes, uint64_t nblk);
 };
@@ -123,8 +130,6 @@ int slot_submit(Device& d, Slot& s, uint64_t bytes, uint64_t nblk, int ht = CIR_
 int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, const uint32_t* len,
                       uint64_t n, uint8_t* out, hipStream_t s, int ht = CIR_HASH_BLAKE2B_256);
 bool valid_hash_type(int ht);
-int ensure_part_streams(Device& d);
-int ensure_relay(Device& d);
 int slot_wait(Device& d, Slot& s);
 
 }  // namespace cir

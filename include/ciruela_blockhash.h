@@ -230,6 +230,16 @@ int cir_debug_hash_uniform_dev(int loader, const void* d_data, uint64_t block_si
  * memory traffic.  bench.py times it as the measured VALU ceiling. */
 int cir_debug_compress_only_dev(uint64_t nlanes, uint32_t lines, uint8_t* d_out, void* stream);
 
+/* Per-part kernel timing of the ordered descriptor batches of ctx's first
+ * device (cir_hash_blocks_dev with a context): enable != 0 starts recording
+ * HIP events around the ordering, the quad part and the lane part of each
+ * batch (at most 256 batches per enable; enabling again restarts), 0 stops.
+ * cir_debug_desc_times waits for the recorded events and returns
+ * out[0] = batches, out[1..3] = summed ordering / quad-part / lane-part
+ * milliseconds, out[4] = summed ordering start -> last part end. */
+int cir_debug_desc_timing(cir_ctx* ctx, int enable);
+int cir_debug_desc_times(cir_ctx* ctx, double out[5]);
+
 /* How many whole blocks of a file of nfull x block_size bytes (plus any short
  * last block) cir_hash_chunks_dev with a context relays on the calling
  * thread's current device (0: none).  Relayed blocks run in quad mode as

@@ -1267,3 +1267,53 @@ def test_relays_from_concurrent_callers(gpu, ctx, oracle):
             want = oracle_chunks(oracle, host, n * bs, bs)
         got = o.cpu().numpy()
         assert first_bad(got, want) is None, (name, first_bad(got, want))
+
+
+@pytest.mark.parametrize("regime", ["lane", "lane_1m", "quad", "quad_1m"])
+def test_desc_relay_unordered_lengths_in_one_bin(gpu, ctx, oracle, regime):
+    """Relayed chains of different lengths that share one length bin of the
+    ordering (order.hip: bins are exact only below 2048 lines, then 16 lines
+    wide at 256 KiB and 64 at 1 MiB), so a group's first chain is not always
+    its longest.  Most chains end on a segment boundary and ~10 % run a few
+    lines past it: before the fix, a group whose first chain ended on the
+    boundary raised the final flag while a longer chain was still unfinished,
+    and that chain's digest was never written (kernels.hip
+    relay_segment).  Descriptors overlap in one small arena (each (offset,
+    length) pair is hashed once by the oracle); every digest is checked."""
+    import torch
+    slots = lane_wave_slots()
+    qslots = slots // 4
+    if regime.startswith("lane"):   # no quad part: > 16384 long chains, lane mode + relay
+        n, extra = slots + slots // 8, slots // 8
+    else:                           # small batch: every chain in the quad part + relay
+        n, extra = 2 * qslots + 2000, 2000
+    base_lines, over = (2048, 15) if not regime.endswith("1m") else (8192, 63)
+    rng = np.random.default_rng(hash(regime) & 0xffff)
+    long_ = rng.random(n) < 0.1
+    lines = np.where(long_, base_lines + rng.integers(1, over + 1, size=n), base_lines)
+    # ragged ends on some of the long chains (still in the same bin)
+    tail = np.where(long_ & (rng.random(n) < 0.5), rng.integers(1, 128, size=n), 0)
+    lens = (lines * 128 - np.where(tail > 0, 128 - tail, 0)).astype(np.int64)
+    offs = 16 * rng.integers(0, 64, size=n)
+    arena_bytes = int(offs.max() + lens.max()) + 64
+    data = dev_random(gpu, arena_bytes, seed=n ^ 0xB1)
+    d_off = torch.tensor(offs, dtype=torch.int64, device="cuda:0")
+    d_len = torch.tensor(lens.astype(np.int32), dtype=torch.int32, device="cuda:0")
+    out = torch.zeros(32 * n, dtype=torch.uint8, device="cuda:0")
+    host = data.cpu().numpy()
+    pairs = sorted(set(zip(offs.tolist(), lens.tolist())))
+    po = np.array([p[0] for p in pairs], dtype=np.uint64)
+    pl = np.array([p[1] for p in pairs], dtype=np.uint32)
+    pd = np.zeros(32 * len(pairs), dtype=np.uint8)
+    oracle.oracle_hash_blocks(host.ctypes.data, po.ctypes.data, pl.ctypes.data, len(pairs),
+                              pd.ctypes.data, 8)
+    index = {p: i for i, p in enumerate(pairs)}
+    sel = np.array([index[(o, ln)] for o, ln in zip(offs.tolist(), lens.tolist())])
+    want = pd.reshape(-1, 32)[sel].reshape(-1)
+    for _ in range(3):  # the order within a bin varies between calls
+        out.zero_()
+        ctx.hash_blocks_dev(data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n,
+                            out.data_ptr(), 0)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        assert first_bad(got, want) is None, "descriptor %s" % first_bad(got, want)

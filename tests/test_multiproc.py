@@ -111,3 +111,25 @@ def test_range_split_gloo(world):
     dig = np.empty(32, dtype=np.uint8)
     lib.oracle_hash_chunks(buf.ctypes.data, BS, BS, dig.ctypes.data, 1)
     assert [int(x) for x in dig] == parts[1][7:]
+
+
+def test_bench_launches_ranks_itself():
+    """`bench.py --gpus 2` with no launcher around it starts two rank
+    processes itself (torch.distributed.run, rendezvous on 127.0.0.1) before
+    touching a GPU; the line reports the process group's own world size and
+    the config-4 workload, and the shards tile [0, 2n)."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--dist-backend", "gloo", "--dry-run", "--steps", "2", "--blocks", "64"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["ranks_seen"] == 2
+    assert rec["config"]["workload"] == "config4"
+    assert sorted(map(tuple, rec["shards"])) == [(0, 64), (64, 64)]

@@ -60,9 +60,15 @@ for s in "$@"; do
     smoke)
       step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests)
-      step tests 900 python -m pytest tests -q -m gpu -x -p no:cacheprovider \
+      step tests 1100 python -u -m pytest tests -v -m gpu -x -p no:cacheprovider \
+        --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} \
         --junitxml=gpurun_out/pytest_gpu.xml > gpurun_out/pytest_gpu.log 2>&1
-      tail -5 gpurun_out/pytest_gpu.log ;;
+      grep -E "PASS|FAIL|ERROR|SKIP" gpurun_out/pytest_gpu.log | tail -15
+      tail -3 gpurun_out/pytest_gpu.log ;;
+    dist2)  # bench.py launching two ranks itself (gloo: they share the one GPU)
+      step dist2 600 python bench.py --gpus 2 --dist-backend gloo --steps 5 --warmup 1 \
+        --blocks "${DIST_BLOCKS:-262144}" > gpurun_out/dist2.json 2> gpurun_out/dist2.err
+      cat gpurun_out/dist2.json ;;
     bench)
       step bench 600 python bench.py --steps 20 --warmup 3 > gpurun_out/bench.json \
         2> gpurun_out/bench.err
