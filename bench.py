@@ -508,14 +508,49 @@ def make_tree(root, gib, file_mib=32, ndirs=40, seed=0x5EED0005):
     return nfiles
 
 
+def tree_read_pass(root, threads=16, piece=4 << 20):
+    """One plain CPU read of every file under root (threads x pread into
+    reused buffers, no GPU): (bytes, seconds)."""
+    from concurrent.futures import ThreadPoolExecutor
+    paths = sorted(os.path.join(dp, f) for dp, _, fs in os.walk(root) for f in fs)
+    bufs = [bytearray(piece) for _ in range(threads)]
+
+    def work(k):
+        mv, n = memoryview(bufs[k]), 0
+        for p in paths[k::threads]:
+            fd = os.open(p, os.O_RDONLY)
+            try:
+                off = 0
+                while True:
+                    r = os.preadv(fd, [mv], off)
+                    if r <= 0:
+                        break
+                    off += r
+                    n += r
+            finally:
+                os.close(fd)
+        return n
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        total = sum(ex.map(work, range(threads)))
+    return total, time.perf_counter() - t0
+
+
 def run_config5(args, ca, ctx, ctx_init_s=None):
     """value = best of the scans; value_first = the first scan of this
     process, which is what one `ciruela sync` sees (it scans once per run,
-    src/client/sync/mod.rs:192-201)."""
+    src/client/sync/mod.rs:192-201).  A tmpfs tree that was just written
+    reads ~6x slower the first time, for any reader (tools/first_read_probe.py:
+    a plain 16-thread CPU read pass 16 GiB/s first, 100-150 after); that
+    cost is paid here by one timed CPU read pass (tree_first_read) before the
+    scans, so seconds_first is the library's first scan, not the OS's first
+    touch of fresh pages."""
     t0 = time.perf_counter()
     nfiles = make_tree(args.tree_dir, args.tree_gib)
     gen_s = time.perf_counter() - t0
     nbytes = nfiles * 32 * (1 << 20)
+    rd_bytes, rd_s = tree_read_pass(args.tree_dir)
+    rd2_bytes, rd2_s = tree_read_pass(args.tree_dir)
     threads = int(os.environ.get("CIR_SCAN_THREADS", "16"))
     cfg = ca.ScannerConfig.new().threads(threads).add_dir(args.tree_dir, "/")
     times = []
@@ -566,18 +601,19 @@ def run_config5(args, ca, ctx, ctx_init_s=None):
             "files": nfiles, "bytes": nbytes, "index_bytes": len(index),
             "image_id": ca.get_hash(index).hex(), "matches_oracle": index == want,
             "tree_gen_s": round(gen_s, 1), "reader_threads": threads, "tree": args.tree_dir,
+            "tree_first_read": {"seconds": round(rd_s, 3), "value": round(rd_bytes / rd_s / GIB, 2),
+                                "second_pass_value": round(rd2_bytes / rd2_s / GIB, 2),
+                                "note": "plain 16-thread CPU read of the tree before the scans "
+                                        "(no GPU): the first read of freshly written tmpfs "
+                                        "pages, then a second pass"},
             "cpu_baseline": cpu}
 
 
-def run_config1(args, ca, ctx):
-    """100 files / 10 MiB, 10 subdirectories, through the `ciruela-index sync`
-    CLI (the indexing half of `ciruela sync --append`, one process: HIP
-    start-up included) and through v1::scan in this process (warm), checked
-    against the scan oracle; CPU baseline = the CPU indexer restatement on
-    the same tree."""
-    import subprocess
+def make_config1_tree(root):
+    """Config 1 (BASELINE.json configs[0]): 100 files, 10 MiB in total, in 10
+    subdirectories, sizes and bytes from numpy default_rng(1).  Returns the
+    byte total."""
     import numpy as np
-    root = "/tmp/ciruela_cfg1_tree"
     rng = np.random.default_rng(1)
     sizes = rng.integers(1, 2 * (10 << 20) // 100, size=100)
     sizes = (sizes * ((10 << 20) / sizes.sum())).astype(np.int64)
@@ -587,7 +623,18 @@ def run_config1(args, ca, ctx):
         os.makedirs(d, exist_ok=True)
         with open(os.path.join(d, "file%03d" % i), "wb") as f:
             f.write(rng.integers(0, 256, size=int(sz), dtype=np.uint8).tobytes())
-    total = int(sizes.sum())
+    return int(sizes.sum())
+
+
+def run_config1(args, ca, ctx):
+    """100 files / 10 MiB, 10 subdirectories, through the `ciruela-index sync`
+    CLI (the indexing half of `ciruela sync --append`, one process: HIP
+    start-up included) and through v1::scan in this process (warm), checked
+    against the scan oracle; CPU baseline = the CPU indexer restatement on
+    the same tree."""
+    import subprocess
+    root = "/tmp/ciruela_cfg1_tree"
+    total = make_config1_tree(root)
     cli = os.path.join(ROOT, "bin", "ciruela-index")
     t0 = time.perf_counter()
     out = subprocess.check_output([cli, "sync", "--append", root + ":/bench"])

@@ -38,30 +38,6 @@ __device__ __forceinline__ uint64_t mk64_pair(uint32_t lo, uint32_t hi) {
   return __builtin_bit_cast(uint64_t, v);
 }
 
-// rotr64(a ^ b, N) on 32-bit halves.  MODE selects the instruction form
-// (gfx950 issue costs measured by tools/valu_ubench.hip, profiles/):
-//   MODE 0: v_alignbit_b32 x2            (any N)
-//   MODE 1: v_perm_b32 x2                (N = 16, 24: byte rotates)
-//   MODE 2: (x << 1) + (x >> 63) as one v_lshl_add_u64 + v_lshrrev_b32 (N = 63)
-template <int N, int MODE>
-__device__ __forceinline__ uint64_t xor_rotr(uint64_t a, uint64_t b) {
-  const uint32_t l = lo32(a) ^ lo32(b), h = hi32(a) ^ hi32(b);
-  if constexpr (N == 32) {
-    return mk64(h, l);
-  } else if constexpr (MODE == 1 && (N == 16 || N == 24)) {
-    // bytes of {S0, S1} numbered S1 = 0..3, S0 = 4..7; result byte k = sel[k]
-    constexpr uint32_t sel = N == 16 ? 0x05040302u : 0x06050403u;
-    return mk64(__builtin_amdgcn_perm(h, l, sel), __builtin_amdgcn_perm(l, h, sel));
-  } else if constexpr (MODE == 2 && N == 63) {
-    const uint64_t x = mk64(l, h);
-    return (x << 1) + (uint64_t)(h >> 31);
-  } else if constexpr (N < 32) {
-    return mk64(__builtin_amdgcn_alignbit(h, l, N), __builtin_amdgcn_alignbit(l, h, N));
-  } else {
-    return mk64(__builtin_amdgcn_alignbit(l, h, N - 32), __builtin_amdgcn_alignbit(h, l, N - 32));
-  }
-}
-
 // a ^ b ^ c on both halves: one full-rate v_bitop3_b32 per half (gfx950).
 __device__ __forceinline__ uint64_t xor3(uint64_t a, uint64_t b, uint64_t c) {
   return mk64(__builtin_amdgcn_bitop3_b32(lo32(a), lo32(b), lo32(c), 0x96),
@@ -80,59 +56,6 @@ __device__ __forceinline__ uint64_t xor3(uint64_t a, uint64_t b, uint64_t c) {
 // fanout = 1, depth = 1 (RFC 7693 section 2.5).
 #define CIR_P0_256 0x01010020ULL
 
-#define CIR_G(a, b, c, d, x, y)   \
-  a = a + b + (x);                \
-  d = xor_rotr<32, 0>(d, a);      \
-  c = c + d;                      \
-  b = xor_rotr<24, R24>(b, c);    \
-  a = a + b + (y);                \
-  d = xor_rotr<16, R16>(d, a);    \
-  c = c + d;                      \
-  b = xor_rotr<63, R63>(b, c);
-
-#define CIR_ROUND(s0, s1, s2, s3, s4, s5, s6, s7, s8, s9, s10, s11, s12, s13, s14, s15) \
-  CIR_G(v0, v4, v8, v12, m[s0], m[s1])                                                   \
-  CIR_G(v1, v5, v9, v13, m[s2], m[s3])                                                   \
-  CIR_G(v2, v6, v10, v14, m[s4], m[s5])                                                  \
-  CIR_G(v3, v7, v11, v15, m[s6], m[s7])                                                  \
-  CIR_G(v0, v5, v10, v15, m[s8], m[s9])                                                  \
-  CIR_G(v1, v6, v11, v12, m[s10], m[s11])                                                \
-  CIR_G(v2, v7, v8, v13, m[s12], m[s13])                                                 \
-  CIR_G(v3, v4, v9, v14, m[s14], m[s15])
-
-// F(h, m, t, f) of RFC 7693 section 3.2 with t < 2^64 (t[1] == 0: a block
-// is at most 2^32 bytes here) and f0 = last ? ~0 : 0, f1 = 0.
-// R16 / R24 / R63: instruction form of the three non-trivial rotates.
-template <int R16, int R24, int R63>
-__device__ __forceinline__ void compress_v(uint64_t h[8], const uint64_t m[16], uint64_t t,
-                                           bool last) {
-  uint64_t v0 = h[0], v1 = h[1], v2 = h[2], v3 = h[3];
-  uint64_t v4 = h[4], v5 = h[5], v6 = h[6], v7 = h[7];
-  uint64_t v8 = CIR_IV0, v9 = CIR_IV1, v10 = CIR_IV2, v11 = CIR_IV3;
-  uint64_t v12 = CIR_IV4 ^ t, v13 = CIR_IV5;
-  uint64_t v14 = last ? ~CIR_IV6 : CIR_IV6, v15 = CIR_IV7;
-  CIR_ROUND(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
-  CIR_ROUND(14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3)
-  CIR_ROUND(11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4)
-  CIR_ROUND(7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8)
-  CIR_ROUND(9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13)
-  CIR_ROUND(2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9)
-  CIR_ROUND(12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11)
-  CIR_ROUND(13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10)
-  CIR_ROUND(6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5)
-  CIR_ROUND(10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0)
-  CIR_ROUND(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
-  CIR_ROUND(14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3)
-  h[0] = xor3(h[0], v0, v8);
-  h[1] = xor3(h[1], v1, v9);
-  h[2] = xor3(h[2], v2, v10);
-  h[3] = xor3(h[3], v3, v11);
-  h[4] = xor3(h[4], v4, v12);
-  h[5] = xor3(h[5], v5, v13);
-  h[6] = xor3(h[6], v6, v14);
-  h[7] = xor3(h[7], v7, v15);
-}
-
 // ---------------------------------------------------------------------------
 // Step-major compression (the production form).  gfx950 issues the 32-bit
 // xor at 2 cycles per wave64 and the 64-bit add / funnel shift at 4
@@ -141,7 +64,8 @@ __device__ __forceinline__ void compress_v(uint64_t h[8], const uint64_t m[16], 
 // its 4 independent columns (or diagonals) at a time, and a scheduling
 // barrier at every change of class keeps the compiler from re-interleaving:
 // 8 slow | 8 fast | 4 slow | 8 fast | 16 slow | 8 fast | 12 slow | 8 fast |
-// 8 slow.  Same instructions as compress_v; 4 % faster register-only
+// 8 slow.  Same instructions as the G-at-a-time order the compiler picks
+// (compress_v, kept in tools/blake2b_variants.hpp); 4 % faster register-only
 // (tools/order_ubench.hip).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
@@ -231,72 +155,9 @@ __device__ __forceinline__ void compress_sm(uint64_t h[8], const uint64_t m[16],
   h[7] = xor3(h[7], v7, v15);
 }
 
-#ifndef CIR_COMPRESS_SM
-#define CIR_COMPRESS_SM 1
-#endif
-
 __device__ __forceinline__ void compress(uint64_t h[8], const uint64_t m[16], uint64_t t,
                                          bool last) {
-#if CIR_COMPRESS_SM
   compress_sm(h, m, t, last);
-#else
-  compress_v<0, 0, 0>(h, m, t, last);
-#endif
-}
-
-// Two independent chains interleaved (ILP 8); same rounds as compress_v.
-#define CIR_G2(a, b, c, d, x, y, A, B, C, D, X, Y) \
-  a = a + b + (x);                                  \
-  A = A + B + (X);                                  \
-  d = xor_rotr<32, 0>(d, a);                        \
-  D = xor_rotr<32, 0>(D, A);                        \
-  c = c + d;                                        \
-  C = C + D;                                        \
-  b = xor_rotr<24, 0>(b, c);                        \
-  B = xor_rotr<24, 0>(B, C);                        \
-  a = a + b + (y);                                  \
-  A = A + B + (Y);                                  \
-  d = xor_rotr<16, 0>(d, a);                        \
-  D = xor_rotr<16, 0>(D, A);                        \
-  c = c + d;                                        \
-  C = C + D;                                        \
-  b = xor_rotr<63, 0>(b, c);                        \
-  B = xor_rotr<63, 0>(B, C);
-
-#define CIR_ROUND2(s0, s1, s2, s3, s4, s5, s6, s7, s8, s9, s10, s11, s12, s13, s14, s15)          \
-  CIR_G2(v0, v4, v8, v12, m[s0], m[s1], w0, w4, w8, w12, q[s0], q[s1])                             \
-  CIR_G2(v1, v5, v9, v13, m[s2], m[s3], w1, w5, w9, w13, q[s2], q[s3])                             \
-  CIR_G2(v2, v6, v10, v14, m[s4], m[s5], w2, w6, w10, w14, q[s4], q[s5])                           \
-  CIR_G2(v3, v7, v11, v15, m[s6], m[s7], w3, w7, w11, w15, q[s6], q[s7])                           \
-  CIR_G2(v0, v5, v10, v15, m[s8], m[s9], w0, w5, w10, w15, q[s8], q[s9])                           \
-  CIR_G2(v1, v6, v11, v12, m[s10], m[s11], w1, w6, w11, w12, q[s10], q[s11])                       \
-  CIR_G2(v2, v7, v8, v13, m[s12], m[s13], w2, w7, w8, w13, q[s12], q[s13])                         \
-  CIR_G2(v3, v4, v9, v14, m[s14], m[s15], w3, w4, w9, w14, q[s14], q[s15])
-
-__device__ __forceinline__ void compress2(uint64_t h[8], const uint64_t m[16], uint64_t g[8],
-                                          const uint64_t q[16], uint64_t t, bool last) {
-  uint64_t v0 = h[0], v1 = h[1], v2 = h[2], v3 = h[3], v4 = h[4], v5 = h[5], v6 = h[6], v7 = h[7];
-  uint64_t v8 = CIR_IV0, v9 = CIR_IV1, v10 = CIR_IV2, v11 = CIR_IV3;
-  uint64_t v12 = CIR_IV4 ^ t, v13 = CIR_IV5, v14 = last ? ~CIR_IV6 : CIR_IV6, v15 = CIR_IV7;
-  uint64_t w0 = g[0], w1 = g[1], w2 = g[2], w3 = g[3], w4 = g[4], w5 = g[5], w6 = g[6], w7 = g[7];
-  uint64_t w8 = CIR_IV0, w9 = CIR_IV1, w10 = CIR_IV2, w11 = CIR_IV3;
-  uint64_t w12 = CIR_IV4 ^ t, w13 = CIR_IV5, w14 = last ? ~CIR_IV6 : CIR_IV6, w15 = CIR_IV7;
-  CIR_ROUND2(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
-  CIR_ROUND2(14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3)
-  CIR_ROUND2(11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4)
-  CIR_ROUND2(7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8)
-  CIR_ROUND2(9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13)
-  CIR_ROUND2(2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9)
-  CIR_ROUND2(12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11)
-  CIR_ROUND2(13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10)
-  CIR_ROUND2(6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5)
-  CIR_ROUND2(10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0)
-  CIR_ROUND2(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
-  CIR_ROUND2(14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3)
-  h[0] ^= v0 ^ v8; h[1] ^= v1 ^ v9; h[2] ^= v2 ^ v10; h[3] ^= v3 ^ v11;
-  h[4] ^= v4 ^ v12; h[5] ^= v5 ^ v13; h[6] ^= v6 ^ v14; h[7] ^= v7 ^ v15;
-  g[0] ^= w0 ^ w8; g[1] ^= w1 ^ w9; g[2] ^= w2 ^ w10; g[3] ^= w3 ^ w11;
-  g[4] ^= w4 ^ w12; g[5] ^= w5 ^ w13; g[6] ^= w6 ^ w14; g[7] ^= w7 ^ w15;
 }
 
 __device__ __forceinline__ void init_state(uint64_t h[8]) {
@@ -466,60 +327,23 @@ template <int CTRL>
 __device__ __forceinline__ uint32_t qd(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
 }
-// Whole 64-bit value into registers (v_mov_b32_dpp x2; no "old" operand).
-template <int CTRL>
-__device__ __forceinline__ uint64_t qperm(uint64_t x) {
-  return mk64((uint32_t)__builtin_amdgcn_mov_dpp((int)lo32(x), CTRL, 0xf, 0xf, false),
-              (uint32_t)__builtin_amdgcn_mov_dpp((int)hi32(x), CTRL, 0xf, 0xf, false));
-}
 constexpr int kQuadFromNext = 0x39;   // lane i <- lane i+1  (quad_perm [1,2,3,0])
 constexpr int kQuadFromNext2 = 0x4E;  // lane i <- lane i+2  (quad_perm [2,3,0,1])
 constexpr int kQuadFromPrev = 0x93;   // lane i <- lane i+3  (quad_perm [3,0,1,2])
 
-// One G of quad mode.  The state arrives in the layout of the previous half
-// round; PB / PC / PD (0 = own lane) name the lanes b, c, d are read from,
-// so the column <-> diagonal moves happen inside this G: b and c are
-// permuted into registers (both feed 64-bit adds, which have no DPP form),
-// d is permuted inside its first consumer, the xor of the rotr-32 step.
-// (a + m) + b: the message add does not wait for b.
-template <int PB, int PC, int PD>
-__device__ __forceinline__ void g_quad(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d,
-                                       uint64_t x, uint64_t y) {
-  a = a + x;
-  if constexpr (PB != 0) b = qperm<PB>(b);
-  if constexpr (PC != 0) c = qperm<PC>(c);
-  a = a + b;
-  uint32_t dl, dh;  // rotr32(d ^ a): swap the halves
-  if constexpr (PD != 0) {
-    dl = qd<PD>(hi32(d)) ^ hi32(a);
-    dh = qd<PD>(lo32(d)) ^ lo32(a);
-  } else {
-    dl = hi32(d) ^ hi32(a);
-    dh = lo32(d) ^ lo32(a);
-  }
-  d = mk64(dl, dh);
-  c = c + d;
-  b = xor_rotr<24, 0>(b, c);
-  a = (a + y) + b;
-  {
-    // the rotate's halves built as a vector, not (hi << 32) | lo: the
-    // compiler then keeps them as one register pair instead of adding them
-    // into c separately (an extra 64-bit add and a move per G)
-    const uint32_t l = lo32(d) ^ lo32(a), h = hi32(d) ^ hi32(a);
-    d = mk64_pair(__builtin_amdgcn_alignbit(h, l, 16), __builtin_amdgcn_alignbit(l, h, 16));
-  }
-  c = c + d;
-  b = xor_rotr<63, 0>(b, c);
-}
-
-// The same G in hand-ordered asm (CIR_QUAD_ASM, the default): the permuted
-// b and c feed their 64-bit adds directly as VOP2 DPP carry pairs
-// (v_add_co_u32_dpp + v_addc_co_u32_dpp) and b's second read is a
-// v_xor_b32_dpp, so no value is moved across lanes on its own: 22 VALU
-// instructions per G instead of 24 (6-7 % less latency per compression,
-// tools/quad_dpp_ubench.hip).  One asm block is a whole compression
-// (compress_quad_asm, message words in registers) or a whole round
-// (round_quad_asm): the compiler puts an s_nop between two inline-asm blocks.
+// One G of quad mode in hand-ordered asm.  The state arrives in the layout of
+// the previous half round; the column <-> diagonal moves happen inside the G:
+// the permuted b and c feed their 64-bit adds directly as VOP2 DPP carry
+// pairs (v_add_co_u32_dpp + v_addc_co_u32_dpp; VOP3 v_lshl_add_u64 has no DPP
+// form on gfx9) and b's second read is a v_xor_b32_dpp, so no value is moved
+// across lanes on its own: 22 VALU instructions per G (the compiled form
+// was 24, ~680 per compression before the DPP folding; 6-7 % less latency
+// per compression, tools/quad_dpp_ubench.hip).  Two DPP adds per step is the
+// minimum under the gfx9 DPP hazard rule (a DPP source must be written >= 2
+// instructions earlier): every 2-step frame assignment of the rows was
+// searched.  One asm block is a whole compression
+// (compress_quad_asm, message words in registers): the compiler puts an
+// s_nop between two inline-asm blocks.
 // a, b, c, d, t (the rotr-32 result) and u (xor scratch) are pinned to
 // v[40:51] so that every block names the same registers; the compiler cannot
 // see the DPP reads inside the asm, so the blocks keep the DPP read-after-
@@ -528,19 +352,13 @@ __device__ __forceinline__ void g_quad(uint64_t& a, uint64_t& b, uint64_t& c, ui
 // (2 wait states, the gfx9 DPP rule); c and d are read across lanes >= 5
 // instructions after their writes.  The last round ends with s_nop 1 for the
 // compiler-generated DPP reads of the finalisation.
-#ifndef CIR_QUAD_ASM
-#define CIR_QUAD_ASM 1
-#endif
-constexpr bool kQuadAsm = CIR_QUAD_ASM != 0;
 // Every quad-mode asm block starts its 8-byte instructions on an 8-byte
 // boundary (the assembler pads with one s_nop 0 when needed; inside the
 // blocks the 4-byte instructions come in pairs).  A VOP2 DPP instruction
 // that straddles it issues ~10 % slower for a wave alone
 // (tools/align_ubench.hip), and the quad kernels moved 7-10 % with nothing
 // but their code offset (profiles/r02/quad_fast/ab_fastpad.log).
-#ifndef CIR_QALIGN
 #define CIR_QALIGN ".p2align 3\n"
-#endif
 #define CIR_QP_39 " quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf"
 #define CIR_QP_4E " quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"
 #define CIR_QP_93 " quad_perm:[3,0,1,2] row_mask:0xf bank_mask:0xf"
@@ -581,16 +399,6 @@ constexpr bool kQuadAsm = CIR_QUAD_ASM != 0;
   "v_xor_b32_dpp v51, v43, v45" PB "\n"                                       \
   "v_alignbit_b32 v42, v51, v50, 24\n"                                        \
   "v_alignbit_b32 v43, v50, v51, 24\n" CIR_QG_TAIL(Y)
-// diagonal step: b, c, d from lanes i+1, i+2, i+3; column step (rounds >= 1):
-// back from lanes i+3, i+2, i+1
-#define CIR_QG_DIAG CIR_QG_DPP(CIR_QP_39, CIR_QP_4E, CIR_QP_93, "%[x1]", "%[y1]")
-#define CIR_QG_COL CIR_QG_DPP(CIR_QP_93, CIR_QP_4E, CIR_QP_39, "%[x0]", "%[y0]")
-#define CIR_QG_OPS                                                            \
-  : "+{v[40:41]}"(a), "+{v[42:43]}"(b), "+{v[44:45]}"(c), "+{v[46:47]}"(d),   \
-    "=&{v[48:49]}"(t), "=&{v[50:51]}"(u)                                      \
-  : [x0] "v"(x0), [y0] "v"(y0), [x1] "v"(x1), [y1] "v"(y1)                    \
-  : "vcc"
-
 // Whole compression in one block (message words prefetched into registers:
 // no s_nop between rounds).  Word k of the schedule is operand m(k mod 40):
 // rounds 10 and 11 repeat rounds 0 and 1.
@@ -707,86 +515,6 @@ __device__ __forceinline__ void compress_quad_fast(uint64_t& h0, uint64_t& h1, u
                  [wr] "v"(wr), [cv] "v"(cv), [dl] "v"(dl), [dh] "v"(dh), [t] "s"(t),
                  [lm] "v"(m0), [step] "s"(step)
                : "vcc", "memory");
-}
-
-// One round of quad mode: column step (words x0, y0), diagonal step (x1, y1).
-// kFirst: round 0 (state in the column layout); kLast: round 11.
-template <bool kFirst, bool kLast>
-__device__ __forceinline__ void round_quad_asm(uint64_t& a, uint64_t& b, uint64_t& c,
-                                               uint64_t& d, uint64_t x0, uint64_t y0,
-                                               uint64_t x1, uint64_t y1) {
-  uint64_t t, u;
-  if constexpr (kFirst)
-    asm volatile(CIR_QALIGN CIR_QG_PLAIN("%[x0]", "%[y0]") CIR_QG_DIAG CIR_QG_OPS);
-  else if constexpr (kLast)
-    asm volatile(CIR_QALIGN CIR_QG_COL CIR_QG_DIAG "s_nop 1\n" CIR_QG_OPS);
-  else
-    asm volatile(CIR_QALIGN CIR_QG_COL CIR_QG_DIAG CIR_QG_OPS);
-}
-
-// One compression of the chain owned by this quad.  line = the quad's 128-B
-// message line in LDS; addr[r*4 + k] = byte offset of the k-th word lane i
-// needs in round r.  cv/dv = IV[i]/IV[4+i]; dmask = this lane's t / final-flag
-// contribution to v[12+i].  kPrefetchAll: issue all 48 LDS reads before the
-// first round (+96 VGPRs) so no round waits on LDS latency.
-// A quad's single wave issues ~1 VALU instruction per 4.3-5 cycles whether
-// or not it depends on the previous one (tools/lat_ubench.hip), so the
-// latency of a chain is its instruction count: 20 per G + 4 permutes per
-// layout change, the finalisation reading c, b, d across lanes.
-template <bool kPrefetchAll, bool kAsm = kQuadAsm>
-__device__ __forceinline__ void compress_quad_t(uint64_t& h0, uint64_t& h1, const uint8_t* line,
-                                                const uint32_t (&addr)[48], uint64_t cv,
-                                                uint64_t dv) {
-  uint64_t a = h0, b = h1, c = cv, d = dv;
-  // rounds 10 and 11 repeat the schedules of rounds 0 and 1: 40 distinct
-  // (round, position) words per lane
-  uint64_t msg[kPrefetchAll ? 40 : 1];
-  if constexpr (kPrefetchAll) {
-#pragma unroll
-    for (int k = 0; k < 40; ++k) msg[k] = *reinterpret_cast<const uint64_t*>(line + addr[k]);
-    // consume every word here: the scheduler cannot sink the reads back into
-    // the rounds, so the compression waits on LDS once instead of per round
-#pragma unroll
-    for (int k = 0; k < 40; ++k) asm volatile("" : "+v"(msg[k]));
-  }
-  auto word = [&](int k) -> uint64_t {
-    if constexpr (kPrefetchAll)
-      return msg[k < 40 ? k : k - 40];
-    else
-      return *reinterpret_cast<const uint64_t*>(line + addr[k]);
-  };
-  if constexpr (kAsm && kPrefetchAll) {
-    compress_quad_asm(a, b, c, d, msg);
-  } else if constexpr (kAsm) {
-    round_quad_asm<true, false>(a, b, c, d, word(0), word(1), word(2), word(3));
-#pragma unroll
-    for (int r = 1; r < 11; ++r)
-      round_quad_asm<false, false>(a, b, c, d, word(4 * r), word(4 * r + 1), word(4 * r + 2),
-                                   word(4 * r + 3));
-    round_quad_asm<false, true>(a, b, c, d, word(44), word(45), word(46), word(47));
-  } else {
-    g_quad<0, 0, 0>(a, b, c, d, word(0), word(1));
-    g_quad<kQuadFromNext, kQuadFromNext2, kQuadFromPrev>(a, b, c, d, word(2), word(3));
-#pragma unroll
-    for (int r = 1; r < 12; ++r) {
-      g_quad<kQuadFromPrev, kQuadFromNext2, kQuadFromNext>(a, b, c, d, word(4 * r + 0),
-                                                           word(4 * r + 1));
-      g_quad<kQuadFromNext, kQuadFromNext2, kQuadFromPrev>(a, b, c, d, word(4 * r + 2),
-                                                           word(4 * r + 3));
-    }
-  }
-  // back to the column layout inside the finalisation: c_i from lane i+2,
-  // b_i from lane i+3, d_i from lane i+1
-  const uint64_t cc = mk64(qd<kQuadFromNext2>(lo32(c)) ^ lo32(a), qd<kQuadFromNext2>(hi32(c)) ^ hi32(a));
-  h0 = h0 ^ cc;
-  const uint64_t bb = mk64(qd<kQuadFromPrev>(lo32(b)) ^ lo32(h1), qd<kQuadFromPrev>(hi32(b)) ^ hi32(h1));
-  h1 = mk64(qd<kQuadFromNext>(lo32(d)) ^ lo32(bb), qd<kQuadFromNext>(hi32(d)) ^ hi32(bb));
-}
-
-__device__ __forceinline__ void compress_quad(uint64_t& h0, uint64_t& h1, const uint8_t* line,
-                                              const uint32_t (&addr)[48], uint64_t cv,
-                                              uint64_t dv) {
-  compress_quad_t<false>(h0, h1, line, addr, cv, dv);
 }
 
 // Software-pipelined quad mode (quad_run's asm path): the 40 message words

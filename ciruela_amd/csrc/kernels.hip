@@ -37,30 +37,10 @@
 #include "uniform.hpp"
 #include "sha512_dev.hpp"
 
-#define CIR_STR2(x) #x
-#define CIR_STR(x) CIR_STR2(x)
-
-#ifndef CIR_QUAD_EXCLUSIVE
-#define CIR_QUAD_EXCLUSIVE 1
-#endif
-
 namespace cir {
 namespace dev {
 
 static inline unsigned grid_for(uint64_t n, uint64_t per) { return (unsigned)((n + per - 1) / per); }
-
-uint64_t quad_small_batch() {
-  static const uint64_t v = [] {
-    const char* e = getenv("CIR_QUAD_SMALL_BATCH");
-    return e ? strtoull(e, nullptr, 10) : kQuadSmallBatch;
-  }();
-  return v;
-}
-
-#ifdef CIR_QUAD_CLOCK
-__device__ unsigned long long g_quad_clock[4];
-__device__ unsigned int g_quad_wave_ticks[16384];  // per wave: blockIdx * 4 + wave
-#endif
 
 // Pure uniform launch: nblk = gridDim.x * 256 equal blocks.
 __global__ __launch_bounds__(kThreads, 5) void k_uniform_glds(const uint8_t* __restrict__ data,
@@ -78,14 +58,11 @@ __global__ __launch_bounds__(kThreads, 5) void k_uniform_glds(const uint8_t* __r
 // and when ngen_wg == 1 the short last block (block nfull) on one lane of
 // workgroup 0 with vector loads (hash_chain_al16).  With a context the short
 // block runs in quad mode on another stream instead (launch_chunks_split).
-// 4 waves per SIMD (128-VGPR budget): the uniform body needs 90 VGPRs, the
-// ragged branch ~100; at 5 (96 VGPRs) the ragged branch spilled 6 VGPRs to
-// scratch.  4 and 5 waves run config 2 within 0.2 % of each other
-// (profiles/r02/ablib_occ4_vs_occ5.log): the body is issue-bound.
-#ifndef CIR_UNI_OCC
-#define CIR_UNI_OCC 4
-#endif
-__global__ __launch_bounds__(kThreads, CIR_UNI_OCC) void k_chunks(const uint8_t* __restrict__ data,
+// 4 waves per SIMD (128-VGPR budget; 107 VGPRs, no spills): at 5 (96 VGPRs)
+// the ragged branch spilled 6 VGPRs to scratch.  4 and 5 waves run config 2
+// within 0.2 % of each other (profiles/r02/ablib_occ4_vs_occ5.log): the body
+// is issue-bound.
+__global__ __launch_bounds__(kThreads, 4) void k_chunks(const uint8_t* __restrict__ data,
                                                          uint64_t nbytes, uint64_t bs,
                                                          uint32_t lines, uint64_t nfull,
                                                          uint32_t ngen_wg,
@@ -205,7 +182,13 @@ __device__ __forceinline__ void quad_init(uint32_t i, uint64_t& h0, uint64_t& h1
 // Advance a quad's chain over L bytes at p, t0 bytes already compressed.
 // final: the last line (partial, or the empty block of an empty input)
 // carries the final flag; otherwise L must be a multiple of 128.
-template <bool kPrefetchAll = false, bool kAsm = kQuadAsm>
+// Pipelined: line it+1 goes regs -> LDS -> the other message set (ma / mb)
+// while line it compresses.  At the top of each half the previous reads have
+// landed (lgkmcnt(0)), so the LDS line is free for the next write and the
+// asm's operands need no wait; the next set's 40 reads stay in flight across
+// the compression (the asm names only the current set).  A compression never
+// waits on the LDS round trip (write, 40 reads: ~300-500 cycles for a wave
+// alone).
 __device__ __forceinline__ void quad_run(uint64_t& h0, uint64_t& h1, uint64_t t0,
                                          const uint8_t* p, uint32_t L, bool active, bool final,
                                          uint8_t* lds, const uint32_t (&addr)[48], uint32_t line,
@@ -222,50 +205,29 @@ __device__ __forceinline__ void quad_run(uint64_t& h0, uint64_t& h1, uint64_t t0
   };
   uint4 u = make_uint4(0, 0, 0, 0), w = u;
   if (total) fetch(0, u, w);
-  if constexpr (kAsm && kPrefetchAll) {
-    // Pipelined: line it+1 goes regs -> LDS -> the other message set (ma /
-    // mb) while line it compresses.  At the top of each half the previous
-    // reads have landed (lgkmcnt(0)), so the LDS line is free for the next
-    // write and the asm's operands need no wait; the next set's 40 reads
-    // stay in flight across the compression (the asm names only the current
-    // set).  A compression no longer waits on the LDS round trip (write, 40
-    // reads: ~300-500 cycles for a wave alone).
-    uint64_t ma[40], mb[40];
-    auto stage = [&](uint32_t it, uint64_t (&m)[40]) {
-      *reinterpret_cast<uint4*>(lds + line + 32u * i) = u;
-      *reinterpret_cast<uint4*>(lds + line + 32u * i + 16u) = w;
-      if (it + 1 < total) fetch(it + 1, u, w);
-      quad_read_msg(m, lds, addr);
-    };
-    auto step = [&](uint32_t it, const uint64_t (&m)[40]) {
-      const bool last = final && it + 1 == total;
-      const uint64_t t = t0 + (last ? (uint64_t)L : (uint64_t)(it + 1) * 128u);
-      const uint64_t dv = dv0 ^ (i == 0 ? t : 0ull) ^ ((i == 2 && last) ? ~0ull : 0ull);
-      compress_quad_regs(h0, h1, m, cv, dv);
-    };
-    constexpr int kLgkm0 = 0xC07F;  // s_waitcnt lgkmcnt(0), vmcnt/expcnt untouched
-    if (total) stage(0, ma);
-    for (uint32_t it = 0; it < total; it += 2) {
-      __builtin_amdgcn_s_waitcnt(kLgkm0);
-      if (it + 1 < total) stage(it + 1, mb);
-      step(it, ma);
-      if (it + 1 >= total) break;
-      __builtin_amdgcn_s_waitcnt(kLgkm0);
-      if (it + 2 < total) stage(it + 2, ma);
-      step(it + 1, mb);
-    }
-    return;
-  }
-  for (uint32_t it = 0; it < total; ++it) {
-    // publish this lane's 32 bytes of the line to its quad (LDS is in order
-    // per wave: the previous compression's reads precede these writes)
+  uint64_t ma[40], mb[40];
+  auto stage = [&](uint32_t it, uint64_t (&m)[40]) {
     *reinterpret_cast<uint4*>(lds + line + 32u * i) = u;
     *reinterpret_cast<uint4*>(lds + line + 32u * i + 16u) = w;
     if (it + 1 < total) fetch(it + 1, u, w);
+    quad_read_msg(m, lds, addr);
+  };
+  auto step = [&](uint32_t it, const uint64_t (&m)[40]) {
     const bool last = final && it + 1 == total;
     const uint64_t t = t0 + (last ? (uint64_t)L : (uint64_t)(it + 1) * 128u);
     const uint64_t dv = dv0 ^ (i == 0 ? t : 0ull) ^ ((i == 2 && last) ? ~0ull : 0ull);
-    compress_quad_t<kPrefetchAll, kAsm>(h0, h1, lds, addr, cv, dv);
+    compress_quad_regs(h0, h1, m, cv, dv);
+  };
+  constexpr int kLgkm0 = 0xC07F;  // s_waitcnt lgkmcnt(0), vmcnt/expcnt untouched
+  if (total) stage(0, ma);
+  for (uint32_t it = 0; it < total; it += 2) {
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+    if (it + 1 < total) stage(it + 1, mb);
+    step(it, ma);
+    if (it + 1 >= total) break;
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+    if (it + 2 < total) stage(it + 2, ma);
+    step(it + 1, mb);
   }
 }
 
@@ -354,12 +316,8 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 
 // Lines of a quad's chain that quad_fast may take: full, not final, from a
 // 16-B aligned start (0 for an inactive quad of the wave: it does not run).
-#ifndef CIR_QUAD_FAST
-#define CIR_QUAD_FAST 1
-#endif
 constexpr uint32_t kQuadFastMin = 8;
 
-template <bool kPrefetchAll, bool kAsm = kQuadAsm>
 __device__ __forceinline__ void quad_chain(bool have, uint64_t b, const uint8_t* p, uint32_t L,
                                            uint8_t* __restrict__ out, uint8_t* lds,
                                            uint32_t wave_lds) {
@@ -370,7 +328,7 @@ __device__ __forceinline__ void quad_chain(bool have, uint64_t b, const uint8_t*
   uint64_t h0, h1;
   quad_init(i, h0, h1);
   uint32_t t0 = 0;
-  if constexpr (CIR_QUAD_FAST && kAsm && kPrefetchAll) {
+  {
     const bool al16 = (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
     const uint32_t nf = !have ? 0xffffffffu : (al16 && L > 0u) ? (L - 1u) >> 7 : 0u;
     const uint32_t nu = wave_min_u32(nf) & ~1u;
@@ -379,8 +337,7 @@ __device__ __forceinline__ void quad_chain(bool have, uint64_t b, const uint8_t*
       t0 = nu * 128u;
     }
   }
-  quad_run<kPrefetchAll, kAsm>(h0, h1, t0, p + t0, have ? L - t0 : 0u, have, true, lds, addr,
-                               line, i);
+  quad_run(h0, h1, t0, p + t0, have ? L - t0 : 0u, have, true, lds, addr, line, i);
   if (have) *reinterpret_cast<uint64_t*>(out + b * 32u + 8u * i) = h0;
 }
 
@@ -393,21 +350,18 @@ __device__ __forceinline__ void quad_single(uint64_t& h0, uint64_t& h1, uint64_t
                                             uint8_t* lds, const uint32_t (&addr)[48],
                                             uint32_t i) {
   uint32_t done = 0;
-  if constexpr (CIR_QUAD_FAST && kQuadAsm) {
-    const bool al16 = (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
-    if (al16 && t0 + n < (1ull << 32)) {
-      const uint32_t nf = final ? (n > 0u ? (n - 1u) >> 7 : 0u) : n >> 7;
-      const uint32_t nu = nf & ~1u;
-      if (nu >= kQuadFastMin) {
-        quad_fast(h0, h1, p, nu, lds, addr, 0u, i, (uint32_t)t0);
-        done = nu * 128u;
-      }
+  const bool al16 = (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+  if (al16 && t0 + n < (1ull << 32)) {
+    const uint32_t nf = final ? (n > 0u ? (n - 1u) >> 7 : 0u) : n >> 7;
+    const uint32_t nu = nf & ~1u;
+    if (nu >= kQuadFastMin) {
+      quad_fast(h0, h1, p, nu, lds, addr, 0u, i, (uint32_t)t0);
+      done = nu * 128u;
     }
   }
-  quad_run<true>(h0, h1, t0 + done, p + done, n - done, true, final, lds, addr, 0u, i);
+  quad_run(h0, h1, t0 + done, p + done, n - done, true, final, lds, addr, 0u, i);
 }
 
-template <bool kPrefetchAll, bool kAsm>
 __device__ __forceinline__ void quad_chains(const uint8_t* __restrict__ arena,
                                             const uint64_t* __restrict__ off,
                                             const uint32_t* __restrict__ len,
@@ -423,7 +377,7 @@ __device__ __forceinline__ void quad_chains(const uint8_t* __restrict__ arena,
     o = off[b];
     L = len[b];
   }
-  quad_chain<kPrefetchAll, kAsm>(have, b, arena + o, L, out, lds, wave_lds);
+  quad_chain(have, b, arena + o, L, out, lds, wave_lds);
 }
 
 // Hashes::hash_file split of one device-resident file, blocks [b0, nblk):
@@ -445,8 +399,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))
   const bool have = b < nblk;
   const uint64_t o = have ? b * bs : 0;
   const uint64_t rest = nbytes - o;
-  quad_chain<true>(have, b, data + o, have ? (uint32_t)(rest < bs ? rest : bs) : 0u, out, lds,
-                   wave * kQuadWaveLds);
+  quad_chain(have, b, data + o, have ? (uint32_t)(rest < bs ? rest : bs) : 0u, out, lds,
+             wave * kQuadWaveLds);
 }
 
 // ---------------------------------------------------------------------------
@@ -468,12 +422,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))
 // flags[g] = segments of group g done (zeroed before the launch).
 // ---------------------------------------------------------------------------
 constexpr uint32_t kRelayGroupChains = 16;
-#ifndef CIR_RELAY_LIGHT
-#define CIR_RELAY_LIGHT 1
-#endif
-#ifndef CIR_RELAY_SLEEP
-#define CIR_RELAY_SLEEP 8  // s_sleep units (64 clocks): ~0.25 us between polls
-#endif
+constexpr int kRelaySleep = 8;  // s_sleep units (64 clocks): ~0.25 us between polls
 // Each segment adds its lines' quad-mode work (~1 us per line) to the lane
 // wave of the SIMD it lands on, so short chains take short segments: at
 // 32 lines, 16-line segments cost the lane part 12 %.  8 = the hand-
@@ -489,14 +438,12 @@ __device__ __forceinline__ void quad_lines(uint64_t& h0, uint64_t& h1, const uin
                                            uint32_t line, uint32_t i) {
   const uint32_t n = l1 - l0;
   uint32_t done = 0;
-  if constexpr (CIR_QUAD_FAST && kQuadAsm) {
-    const uint32_t nu = (final ? n - 1u : n) & ~1u;
-    if (nu >= kQuadFastMin) {
-      if (have) quad_fast(h0, h1, blk + (uint64_t)l0 * 128u, nu, lds, addr, line, i, l0 * 128u);
-      done = nu;
-    }
+  const uint32_t nu = (final ? n - 1u : n) & ~1u;
+  if (nu >= kQuadFastMin) {
+    if (have) quad_fast(h0, h1, blk + (uint64_t)l0 * 128u, nu, lds, addr, line, i, l0 * 128u);
+    done = nu;
   }
-  quad_run<true>(h0, h1, (uint64_t)(l0 + done) * 128u, blk + (uint64_t)(l0 + done) * 128u,
+  quad_run(h0, h1, (uint64_t)(l0 + done) * 128u, blk + (uint64_t)(l0 + done) * 128u,
                  have ? (n - done) * 128u : 0u, have, final, lds, addr, line, i);
 }
 
@@ -586,7 +533,7 @@ __device__ __forceinline__ void relay_segment(const R& r, uint32_t g, uint32_t s
   // lines of this lane's chain in the segment; nu = the wave's common run
   // of full, not final, 16-B aligned lines for the hand-scheduled loop
   uint32_t nu = 0;
-  if constexpr (CIR_QUAD_FAST && kQuadAsm) {
+  {
     const uint32_t c = chain(lane_now());
     uint32_t avail = 0xffffffffu;  // quads without a chain here do not bound it
     if (c < r.n) {
@@ -620,9 +567,11 @@ __device__ __forceinline__ void relay_segment(const R& r, uint32_t g, uint32_t s
           __hip_atomic_load(flags + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
       if (fl == s) break;
       if (k >= max_polls) return;  // the finisher takes over from here
-      __builtin_amdgcn_s_sleep(CIR_RELAY_SLEEP);
+      __builtin_amdgcn_s_sleep(kRelaySleep);
     }
-    if (!CIR_RELAY_LIGHT) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // compiler barrier: the chain-value loads below stay after the flag load
+    // (in the ISA they also depend on it through the scalar branch)
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
   }
   __builtin_amdgcn_s_setprio(3);
   uint64_t h0, h1;
@@ -632,15 +581,10 @@ __device__ __forceinline__ void relay_segment(const R& r, uint32_t g, uint32_t s
       quad_init(lane & 3u, h0, h1);
     } else {
       uint64_t* st = state + ((uint64_t)g * 64u + lane) * 2u;
-      if (CIR_RELAY_LIGHT) {
-        // agent-scope loads (sc1): coherent across XCDs without the L2
-        // invalidate of an acquire fence; issued after the flag was seen
-        h0 = __hip_atomic_load(st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        h1 = __hip_atomic_load(st + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        h0 = st[0];
-        h1 = st[1];
-      }
+      // agent-scope loads (sc1): coherent across XCDs without the L2
+      // invalidate of an acquire fence; issued after the flag was seen
+      h0 = __hip_atomic_load(st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      h1 = __hip_atomic_load(st + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   if (nu) {
@@ -663,8 +607,8 @@ __device__ __forceinline__ void relay_segment(const R& r, uint32_t g, uint32_t s
     }
     uint32_t addr[48];
     quad_addr(addr, (lane >> 2) * 128u, lane & 3u);
-    quad_run<true>(h0, h1, (uint64_t)(l0 + nu) * 128u, p, (uint32_t)L, have, fin, lds, addr,
-                   (lane >> 2) * 128u, lane & 3u);
+    quad_run(h0, h1, (uint64_t)(l0 + nu) * 128u, p, (uint32_t)L, have, fin, lds, addr,
+             (lane >> 2) * 128u, lane & 3u);
   }
   const uint32_t lane = lane_now(), c = chain(lane);
   if (active(c)) {
@@ -672,25 +616,24 @@ __device__ __forceinline__ void relay_segment(const R& r, uint32_t g, uint32_t s
       *reinterpret_cast<uint64_t*>(out + r.block(c) * 32u + 8u * (lane & 3u)) = h0;
     } else {
       uint64_t* st = state + ((uint64_t)g * 64u + lane) * 2u;
-      if (CIR_RELAY_LIGHT) {
-        __hip_atomic_store(st, h0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(st + 1, h1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        st[0] = h0;
-        st[1] = h1;
-      }
+      __hip_atomic_store(st, h0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(st + 1, h1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   if (!publish) return;
-  // the chain values reach every XCD's view before the flag: agent-scope
-  // stores (sc1, written through to the coherent level) completed by
-  // vmcnt(0) -- no L2 write-back of a release fence; the digests are read
-  // only after the kernel (CIR_RELAY_LIGHT=0: the fences of round 2's first
-  // relay)
-  if (CIR_RELAY_LIGHT)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  // The hand-off protocol (fence-free; +1-5 % on relayed shapes against
+  // agent-scope acquire/release fences, which write back / invalidate the
+  // whole L2: profiles/r02/relay/light/).  Its ISA assumptions, checked on
+  // the built code object by tests/test_relay_isa.py:
+  //   * the chain values are stored and loaded with sc1 (agent-scope relaxed
+  //     atomics: written through to, and read from, the level every XCD
+  //     sees);
+  //   * the producer's s_waitcnt vmcnt(0) completes those stores before the
+  //     flag store is issued (gfx9 counts stores in vmcnt, in order);
+  //   * the consumer reads the chain values only after the flag load has
+  //     returned the expected value (the poll loop's scalar branch).
+  // The digests themselves are read only after the kernel.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (lane == 0)
     __hip_atomic_store(flags + g, group_final ? 0xffffffffu : s + 1u, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
@@ -758,16 +701,13 @@ __device__ __forceinline__ bool desc_qrelay_on(const uint32_t* count, const uint
 // relay_extra / relay_min_lines (small batches only): the last relay_extra
 // chains run in k_desc_relay instead when desc_qrelay_on (the base then
 // runs at priority 2 so the relay's segments issue first).
-template <bool kAsm, bool kExclusive>
+template <bool kExclusive>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_quad_long(
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ perm, uint32_t* n_long,
     uint32_t nq_wg, uint8_t* __restrict__ out, uint64_t n, uint32_t relay_extra,
     uint32_t relay_min_lines) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWaves * kQuadWaveLds];
-#ifdef CIR_QPAD  // code-layout probe: CIR_QPAD 4-byte s_nop's ahead of the body
-  asm volatile(".rept " CIR_STR(CIR_QPAD) "\ns_nop 0\n.endr");
-#endif
   if constexpr (kExclusive) {
     asm volatile("v_accvgpr_write_b32 a255, 0" ::: "a255");
     // this workgroup holds its CU: count it for k_gate (n_long[1])
@@ -783,20 +723,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 2))
     __builtin_amdgcn_s_setprio(2);
   else
     __builtin_amdgcn_s_setprio(3);
-#ifdef CIR_QUAD_CLOCK  // diagnostics build: per-wave shader clock / 100 MHz clock
-  const uint64_t c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
-#endif
-  quad_chains<true, kAsm>(arena, off, len, perm, first, nl, out, lds, wave * kQuadWaveLds);
-#ifdef CIR_QUAD_CLOCK
-  const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-  if ((threadIdx.x & 63u) == 0) {
-    atomicAdd(&g_quad_clock[0], (unsigned long long)(c1 - c0));
-    atomicAdd(&g_quad_clock[1], (unsigned long long)(r1 - r0));
-    atomicAdd(&g_quad_clock[2], 1ull);
-    atomicMax(&g_quad_clock[3], (unsigned long long)(r1 - r0));
-    if (blockIdx.x * 4 + wave < 16384) g_quad_wave_ticks[blockIdx.x * 4 + wave] = (unsigned)(r1 - r0);
-  }
-#endif
+  quad_chains(arena, off, len, perm, first, nl, out, lds, wave * kQuadWaveLds);
 }
 
 // The lane part of an exclusive mixed batch waits until every quad
@@ -834,9 +761,7 @@ __global__ void k_gate(const uint32_t* started, uint32_t target, uint32_t max_ro
 // fell to 771); with the hand-scheduled quad loop: 0 886-892, 48 952-957,
 // 60 948-957, 72 937-941, 90 907; after the ordering fixes: 0 908-918, 48
 // 977-993, 64 1012-1021, 80 970-973, 100 930-934.
-#ifndef CIR_LANE_PACE
-#define CIR_LANE_PACE 64
-#endif
+constexpr uint32_t kLanePace = 64;
 
 // Workgroups of a paced lane part, or 0 when the batch is not paced (no
 // pacing asked, no long chain, or more long chains than the quad part holds).
@@ -864,7 +789,7 @@ __device__ __forceinline__ void lane_chain(const uint8_t* __restrict__ arena,
 // spilled around the chain loop, not in it).  With pace != 0 it leaves a
 // paced batch to k_lane_tiles.
 // Relay of a descriptor batch (launch_mixed): the host launches one when
-// the batch is k = 1 .. CIR_RELAY_MAXK lane waves per SIMD plus `extra` chains
+// the batch is k = 1 .. kRelayMaxK lane waves per SIMD plus `extra` chains
 // (extra = n mod slots, slots = 64 x SIMDs); whether it runs is decided on
 // the device, where the lengths are: only with no quad part (no long chains,
 // or more than it holds: then every chain is lane mode and extra is exact),
@@ -1082,10 +1007,7 @@ hipError_t launch_single(const uint8_t* h_src, uint32_t n, uint8_t* d_scratch, u
 // SHA-512/256 over a descriptor batch, one lane per block (dir-signature's
 // HashType::sha512_256()).  5 waves per SIMD: the asm rounds need 93 VGPRs
 // (the compiled ones 168, at 3 waves).
-#ifndef CIR_SHA_OCC
-#define CIR_SHA_OCC (CIR_SHA_ASM ? 5 : 3)
-#endif
-__global__ __launch_bounds__(kThreads, CIR_SHA_OCC) void k_sha_desc(const uint8_t* __restrict__ arena,
+__global__ __launch_bounds__(kThreads, 5) void k_sha_desc(const uint8_t* __restrict__ arena,
                                                            const uint64_t* __restrict__ off,
                                                            const uint32_t* __restrict__ len,
                                                            const uint32_t* __restrict__ perm,
@@ -1226,7 +1148,7 @@ static uint64_t device_simds() {
 // (the small-batch limit) quad mode always.
 static bool chunks_in_quad(uint64_t nblk, uint64_t bs) {
   if (bs < 128ull * kQuadSmallMinLines || bs > 0xffffffffull) return false;
-  if (nblk < quad_small_batch()) return true;
+  if (nblk < kQuadSmallBatch) return true;
   const uint64_t wave_slots = 64ull * device_simds();  // one lane wave per SIMD
   return nblk > wave_slots && nblk * 8 <= wave_slots * 13;
 }
@@ -1260,14 +1182,11 @@ hipError_t launch_chunks(const uint8_t* data, uint64_t nbytes, uint64_t bs, uint
 // chains and trailed the launch; in quad mode it takes about a third of a
 // lane-mode chain's time.  Forked from s (`fork`), joined back (`join`).
 // Falls back to launch_chunks where the split does not apply.
-// CIR_RELAY=0 turns the relay off (A/B); CIR_RELAY_SEGS = the segment waves
-// one relay aims at (default: one per SIMD).
-// Relays run up to 32 whole lane waves per SIMD (17 - 20 measured: 32 KiB x
-// 1114113 blocks 2066-2070 -> 2193 GiB/s, x 1310721 2094-2099 -> 2193-2203,
-// as descriptors +3-5 %; profiles/r02/relay/maxk/).
-#ifndef CIR_RELAY_MAXK
-#define CIR_RELAY_MAXK 32
-#endif
+// A relay aims at one segment wave per SIMD in total (kRelayTargetWaves x
+// SIMDs).  Relays run up to 32 whole lane waves per SIMD (17 - 20 measured:
+// 32 KiB x 1114113 blocks 2066-2070 -> 2193 GiB/s, x 1310721 2094-2099 ->
+// 2193-2203, as descriptors +3-5 %; profiles/r02/relay/maxk/).
+constexpr uint64_t kRelayMaxK = 32;
 // With k >= 3 lane waves per SIMD the lane part is launched with
 // kRelayLanePad bytes of extra LDS per workgroup: two k_chunks workgroups
 // per CU (2 x 64 KiB of 160), so two lane waves per SIMD (2 x 112 VGPRs)
@@ -1281,62 +1200,21 @@ constexpr uint32_t kRelayQuadPad = 73 * 1024;
 // two workgroups per CU.
 constexpr uint32_t kRelayDescLanePad = 64 * 1024;
 
-static bool relay_enabled() {
-  static const bool on = [] {
-    const char* v = getenv("CIR_RELAY");
-    return !(v && v[0] == '0' && v[1] == 0);
-  }();
-  return on;
-}
-
-static uint64_t relay_target_waves(uint64_t simds) {
-  static const uint64_t v = [] {
-    const char* e = getenv("CIR_RELAY_SEGS");
-    return e ? strtoull(e, nullptr, 10) : 0ull;
-  }();
-  return v ? v : simds;
-}
-
-static uint64_t relay_min_quad_k() {  // CIR_RELAY_QMINK: A/B of the quad-regime floor
-  static const uint64_t v = [] {
-    const char* e = getenv("CIR_RELAY_QMINK");
-    return e ? strtoull(e, nullptr, 10) : 1ull;
-  }();
-  return v;
-}
-
-// tuning probes (read per call; diagnostics of the quad-regime rule)
-static uint64_t relay_env(const char* name, uint64_t dflt) {
-  const char* e = getenv(name);
-  return e ? strtoull(e, nullptr, 10) : dflt;
-}
+// The lane-regime cap, in eighths of a lane wave per SIMD (relay_plan,
+// desc_relay_on): beyond 5/8 one more lane wave costs less than the relayed
+// chains' quad-mode work (profiles/r02/relay/).
+constexpr uint64_t kRelayCap8 = 5;
+// The k = 1 quad-regime relay's segments: its chain is as long as the
+// base's and has no slack, so every hand-off adds to it (profiles/r02/relay/qshort/).
+constexpr uint32_t kRelayQuad1Seg = 32;
 
 // Quad regime: extra chains of up to 1/2 of a quad wave per SIMD relay
-// (CIR_RELAY_QFRAC / CIR_RELAY_DQFRAC = d: up to 1/d, chunk form /
-// descriptors); past 1/4 only chains of >= 128 lines (32 KiB x 24576
-// 1283 -> 1535 GiB/s, 1 MiB x 24576 1301 -> 1690; 3/4 is no better than
-// none: profiles/r02/relay/qfrac/).
-static bool quad_relay_fits(uint64_t extra, uint64_t qslots, bool desc) {
-  return extra * relay_env(desc ? "CIR_RELAY_DQFRAC" : "CIR_RELAY_QFRAC", 2) <= qslots;
-}
+// (chunk form and descriptors); past 1/4 only chains of >= 128 lines
+// (32 KiB x 24576 1283 -> 1535 GiB/s, 1 MiB x 24576 1301 -> 1690; 3/4 is no
+// better than none: profiles/r02/relay/qfrac/).
+static bool quad_relay_fits(uint64_t extra, uint64_t qslots) { return extra * 2 <= qslots; }
 static uint32_t quad_relay_min_lines(uint64_t k, uint64_t extra, uint64_t qslots) {
   return extra * 4 > qslots ? 128u : (k == 1 ? 64u : 32u);
-}
-
-static uint32_t relay_quad1_seg() {  // CIR_RELAY_QSEG1: A/B of the k = 1 quad segments
-  static const uint32_t v = [] {
-    const char* e = getenv("CIR_RELAY_QSEG1");
-    return e ? (uint32_t)strtoul(e, nullptr, 10) : 32u;
-  }();
-  return std::max<uint32_t>(v, kRelayMinSegLines);
-}
-
-static uint64_t relay_max_k() {
-  static const uint64_t v = [] {
-    const char* e = getenv("CIR_RELAY_MAXK");
-    return e ? strtoull(e, nullptr, 10) : (uint64_t)CIR_RELAY_MAXK;
-  }();
-  return v;
 }
 
 // How a chunk-form file of nfull whole blocks (+ maybe a short last one)
@@ -1353,7 +1231,7 @@ struct RelayPlan {
   bool relay_first = false;              // enqueue the relay before the base
 };
 
-// Lane regime (nfull >= one lane wave per SIMD): k = 1 .. CIR_RELAY_MAXK whole
+// Lane regime (nfull >= one lane wave per SIMD): k = 1 .. kRelayMaxK whole
 // lane waves per SIMD plus extra blocks up to min(5/8, lines/32) of a lane
 // wave per SIMD (relay_cap_div); beyond that one more lane wave (or the quad band of
 // chunks_in_quad) costs less than the relayed chains' quad-mode work
@@ -1364,15 +1242,14 @@ struct RelayPlan {
 // 16 <= lines, bs < 2^31.
 static bool relay_plan(uint64_t nfull, uint64_t bs, RelayPlan& p) {
   p = RelayPlan();
-  if (!relay_enabled() || bs % 128u != 0 || bs < 128u * 16u || bs >= (1ull << 31)) return false;
+  if (bs % 128u != 0 || bs < 128u * 16u || bs >= (1ull << 31)) return false;
   const uint64_t simds = device_simds(), lines = bs / 128u;
   const uint64_t lane_slots = 64ull * simds, quad_slots = 16ull * simds;
   if (nfull >= lane_slots) {
     const uint64_t k = nfull / lane_slots, extra = nfull % lane_slots;
     const uint64_t cap =
-        std::min(lane_slots * relay_env("CIR_RELAY_CAP8", 5) / 8,
-                 lane_slots * lines / relay_env("CIR_RELAY_CAPDIV", relay_cap_div(lines)));
-    if (k > relay_max_k() || extra == 0 || extra > cap) return false;
+        std::min(lane_slots * kRelayCap8 / 8, lane_slots * lines / relay_cap_div(lines));
+    if (k > kRelayMaxK || extra == 0 || extra > cap) return false;
     p.base = nfull - extra;
     p.nrel = extra;
     p.pad = k > 2 ? kRelayLanePad : 0u;
@@ -1381,9 +1258,9 @@ static bool relay_plan(uint64_t nfull, uint64_t bs, RelayPlan& p) {
     // (profiles/r02/relay/qshort/); past the small-batch limit (k = 3)
     // lane mode takes over from 1/64 of a quad wave of extra blocks on
     const uint64_t k = nfull / quad_slots, extra = nfull % quad_slots;
-    if (extra == 0 || k < relay_min_quad_k() || !quad_relay_fits(extra, quad_slots, false) ||
-        lines < relay_env("CIR_RELAY_QLINES", quad_relay_min_lines(k, extra, quad_slots)) ||
-        (nfull >= quad_small_batch() && extra * 64 > quad_slots))
+    if (extra == 0 || k < 1 || !quad_relay_fits(extra, quad_slots) ||
+        lines < quad_relay_min_lines(k, extra, quad_slots) ||
+        (nfull >= kQuadSmallBatch && extra * 64 > quad_slots))
       return false;
     p.base = nfull - extra;
     p.nrel = extra;
@@ -1393,9 +1270,8 @@ static bool relay_plan(uint64_t nfull, uint64_t bs, RelayPlan& p) {
     // short here) with 8-line segments; at k = 1 it has no slack at all (its
     // chain is as long as the base's and every hand-off adds to it): 32-line
     // segments (profiles/r02/relay/qshort/)
-    p.min_seg = k == 1 ? relay_quad1_seg()
-                       : (uint32_t)relay_env("CIR_RELAY_QSEG", kRelayMinSegLines);
-    p.relay_first = relay_env("CIR_RELAY_QFIRST", 1) != 0;
+    p.min_seg = k == 1 ? kRelayQuad1Seg : kRelayMinSegLines;
+    p.relay_first = true;
   }
   if ((p.nrel + kRelayGroupChains - 1) / kRelayGroupChains > kRelayMaxGroups) return false;
   return true;
@@ -1407,7 +1283,7 @@ uint64_t relay_blocks(uint64_t nfull, uint64_t bs) {
 }
 
 static bool desc_may_relay_slots(uint64_t n, uint64_t slots) {
-  return relay_enabled() && n >= slots && n / slots <= relay_max_k() && n % slots != 0 &&
+  return n >= slots && n / slots <= kRelayMaxK && n % slots != 0 &&
          (n % slots + kRelayGroupChains - 1) / kRelayGroupChains <= kRelayMaxGroups;
 }
 
@@ -1421,7 +1297,7 @@ static hipError_t launch_relay(const uint8_t* data, uint64_t bs, uint64_t b0, ui
   const uint32_t lines = (uint32_t)(bs / 128u);
   const uint32_t groups = (uint32_t)((nrel + kRelayGroupChains - 1) / kRelayGroupChains);
   if (groups > r.groups) return hipErrorInvalidValue;
-  const uint64_t target = relay_target_waves(device_simds());
+  const uint64_t target = device_simds();
   uint32_t nseg = (uint32_t)std::max<uint64_t>(1, target / groups);
   nseg = std::min(nseg, std::max(1u, lines / min_seg));
   uint32_t seg = ((lines + nseg - 1) / nseg + 1u) & ~1u;
@@ -1521,13 +1397,6 @@ hipError_t launch_general_desc(const uint8_t* arena, const uint64_t* off, const 
   return hipGetLastError();
 }
 
-static uint32_t lane_pace() {
-  static const uint32_t pace = [] {  // CIR_LANE_PACE=N overrides (0: no pacing)
-    const char* v = getenv("CIR_LANE_PACE");
-    return v ? (uint32_t)strtoul(v, nullptr, 10) : (uint32_t)CIR_LANE_PACE;
-  }();
-  return pace;
-}
 
 // The descriptor relay (k_desc_relay + its finisher) of the last `extra`
 // chains of an ordered batch on stream st; the kernels decide on the device
@@ -1576,7 +1445,7 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
   // decides on the device whether it runs)
   const uint64_t slots = 64ull * device_simds();
   // the most a lane-regime relay takes, in eighths of a lane wave per SIMD
-  const uint32_t cap8 = (uint32_t)relay_env("CIR_RELAY_DCAP8", 5);
+  const uint32_t cap8 = (uint32_t)kRelayCap8;
   uint32_t extra = 0, groups = 0, nseg_max = 1;
   if (relay && relay->flags && qs != s && aux != qs && desc_may_relay_slots(n, slots)) {
     extra = (uint32_t)(n % slots);
@@ -1584,29 +1453,29 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
     if (groups > relay->groups) {
       extra = 0;
     } else {
-      nseg_max = (uint32_t)std::max<uint64_t>(1, relay_target_waves(device_simds()) / groups);
+      nseg_max = (uint32_t)std::max<uint64_t>(1, device_simds() / groups);
     }
   }
   const uint64_t nq = std::min<uint64_t>((n + 63) / 64, quad_max_wg(n));
   const uint64_t lane_grid = grid_for(n, kThreads);
   if (lane_grid > 0x7fffffffull) return hipErrorInvalidValue;
-  const uint32_t pace = aux != qs ? lane_pace() : 0u;  // only beside a concurrent quad part
-  const bool exclusive = CIR_QUAD_EXCLUSIVE && n >= quad_small_batch();
+  const uint32_t pace = aux != qs ? kLanePace : 0u;  // only beside a concurrent quad part
+  const bool exclusive = n >= kQuadSmallBatch;
   // small batch: a relay of the chains past k whole quad waves per SIMD
   // (desc_qrelay_on decides on the device)
   const uint64_t qslots = 16ull * device_simds();
   uint32_t qextra = 0;
   // (a relay runs only on the device's own quad-part stream, never on the
   // caller's: relays share the device's scratch, one stream orders them)
-  if (!exclusive && relay && relay->flags && relay_enabled() && qs != s && aux != qs &&
+  if (!exclusive && relay && relay->flags && qs != s && aux != qs &&
       n >= qslots &&
-      n % qslots != 0 && quad_relay_fits(n % qslots, qslots, true))
+      n % qslots != 0 && quad_relay_fits(n % qslots, qslots))
     qextra = (uint32_t)(n % qslots);
   // Small batches run both parts on aux, one after the other (the lane part
   // holds only chains of < 8 lines): qs only carries a relay, and without
   // one the fork to qs and the join back cost ~25 us of a 0.4 ms batch
   // (32 KiB x 16384, profiles/r02/desc/serial/)
-  const bool serial = !exclusive && n < quad_small_batch() && qextra == 0;
+  const bool serial = !exclusive && n < kQuadSmallBatch && qextra == 0;
   const bool qs_used = qs != s && !serial;
   hipError_t e = hipEventRecord(fork, s);
   if (e == hipSuccess && qs_used) e = hipStreamWaitEvent(qs, fork, 0);
@@ -1619,7 +1488,7 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
     // taking every SIMD first.
     e = mark(0, qs);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_quad_long<kQuadAsm, true>), dim3((unsigned)nq), dim3(kThreads), 0, qs,
+    hipLaunchKernelGGL((k_quad_long<true>), dim3((unsigned)nq), dim3(kThreads), 0, qs,
                        arena, off, len, perm, n_long, (uint32_t)nq, out, n, 0u, 0u);
     e = hipGetLastError();
     if (e == hipSuccess) e = mark(1, qs);
@@ -1634,7 +1503,7 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
       const uint64_t lane_wgs = std::min<uint64_t>(lane_grid, 2ull * device_simds() / 4ull);
       e = launch_desc_relay(arena, off, len, perm, n, n_long, (uint32_t)nq, extra,
                             (uint32_t)slots, groups, nseg_max, 0u, kRelayMinSegLines, cap8,
-                            relay_env("CIR_RELAY_GATE", 1) ? (uint32_t)lane_wgs : 0u, *relay, out,
+                            (uint32_t)lane_wgs, *relay, out,
                             qs);
       if (e != hipSuccess) return e;
     }
@@ -1673,10 +1542,10 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
       const uint32_t qk = (uint32_t)(n / qslots);
       qmin = quad_relay_min_lines(qk, qextra, qslots);
       const uint32_t qnseg =
-          (uint32_t)std::max<uint64_t>(1, relay_target_waves(device_simds()) / qgroups);
+          (uint32_t)std::max<uint64_t>(1, device_simds() / qgroups);
       e = launch_desc_relay(arena, off, len, perm, n, n_long, (uint32_t)nq, qextra,
                             (uint32_t)qslots, qgroups, qnseg, qmin,
-                            qk == 1 ? relay_quad1_seg() : kRelayMinSegLines, 0u, 0u, *relay,
+                            qk == 1 ? kRelayQuad1Seg : kRelayMinSegLines, 0u, 0u, *relay,
                             out, qs);
       if (e != hipSuccess) return e;
     }
@@ -1690,7 +1559,7 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
     hipStream_t qst = qs_used && !qextra ? qs : aux;
     e = mark(0, qst);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_quad_long<kQuadAsm, false>), dim3((unsigned)nq), dim3(kThreads),
+    hipLaunchKernelGGL((k_quad_long<false>), dim3((unsigned)nq), dim3(kThreads),
                        qextra ? kRelayQuadPad : 0u, qst, arena, off, len, perm, n_long,
                        (uint32_t)nq, out, n, qextra, qmin);
     e = hipGetLastError();
@@ -1717,17 +1586,3 @@ hipError_t launch_fill_splitmix64(uint64_t* p, uint64_t nwords, uint64_t seed,
 
 }  // namespace dev
 }  // namespace cir
-
-#ifdef CIR_QUAD_CLOCK
-// Diagnostics build only: sums of the quad waves' (shader cycles, 100 MHz
-// ticks, waves) and the longest wave's ticks since the last call; resets them.
-extern "C" int cir_debug_quad_clock(unsigned long long* out4) {
-  if (hipMemcpyFromSymbol(out4, HIP_SYMBOL(cir::dev::g_quad_clock), 32) != hipSuccess) return -1;
-  static const unsigned long long zero[4] = {0, 0, 0, 0};
-  return hipMemcpyToSymbol(HIP_SYMBOL(cir::dev::g_quad_clock), zero, 32) == hipSuccess ? 0 : -1;
-}
-extern "C" int cir_debug_quad_wave_ticks(unsigned* out, unsigned n) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(cir::dev::g_quad_wave_ticks), 4ull * (n < 16384 ? n : 16384)) ==
-                 hipSuccess ? 0 : -1;
-}
-#endif

@@ -14,10 +14,7 @@ enum class Loader : int { kGlds = 0, kDirect = 1 };
 // config 3 A/B (profiles/r01/cfg3_quad_threshold.log): 2048 lines 659 GiB/s,
 // 1024 782, 512 760, 256 769 -- below 2048, the ragged 1 MiB blocks no
 // longer trail the lane kernel.
-#ifndef CIR_QUAD_MIN_LINES
-#define CIR_QUAD_MIN_LINES 1024
-#endif
-constexpr uint32_t kQuadMinLines = CIR_QUAD_MIN_LINES;
+constexpr uint32_t kQuadMinLines = 1024;
 constexpr int kQuadMaxWg = 256;  // at most 256 x 64 = 16384 chains in quad mode
 
 // Small batches: lane mode is latency-bound below about one wave per SIMD
@@ -29,19 +26,13 @@ constexpr int kQuadMaxWg = 256;  // at most 256 x 64 = 16384 chains in quad mode
 // modes cross at ~49152 chains (within 4 % there at 32 KiB, 256 KiB and
 // 1 MiB); at 65535 lane mode is ahead (1606 vs 1438 GiB/s at 32 KiB, 1916
 // vs 1703 at 256 KiB; profiles/r01/quad_asm_ab.md).
-#ifndef CIR_QUAD_SMALL_BATCH
-#define CIR_QUAD_SMALL_BATCH 49153
-#endif
-constexpr uint64_t kQuadSmallBatch = CIR_QUAD_SMALL_BATCH;
+constexpr uint64_t kQuadSmallBatch = 49153;
 constexpr uint32_t kQuadSmallMinLines = 8;
-// kQuadSmallBatch, or CIR_QUAD_SMALL_BATCH from the environment (read once;
-// a tuning probe for tools/ and the shape sweeps)
-uint64_t quad_small_batch();
 inline uint32_t quad_min_lines(uint64_t n) {
-  return n < quad_small_batch() ? kQuadSmallMinLines : kQuadMinLines;
+  return n < kQuadSmallBatch ? kQuadSmallMinLines : kQuadMinLines;
 }
 inline uint64_t quad_max_wg(uint64_t n) {
-  return n < quad_small_batch() ? (n + 63) / 64 : (uint64_t)kQuadMaxWg;
+  return n < kQuadSmallBatch ? (n + 63) / 64 : (uint64_t)kQuadMaxWg;
 }
 
 // nblk equal blocks of bs bytes at data (bs % 128 == 0, data 16-byte aligned,

@@ -11,24 +11,16 @@
 //   k_order_place  each workgroup scans the histogram (descending bins),
 //                  reserves its chunk's slots per bin with one atomic per
 //                  used bin, and places its chains through LDS cursors.
-// hipCUB's radix sort on 16-bit keys (CIR_ORDER_CUB=1) took ~10 launches:
-// ~0.13 ms with one context per process, ~0.5 ms with four (each launch
-// ~50 us once several contexts' streams share the hardware queues;
-// profiles/r02/early_quad/).
-#include <hipcub/hipcub.hpp>
-
+// Round 1-2 used hipCUB's radix sort on 16-bit keys: ~10 launches, ~0.13 ms
+// with one context per process, ~0.5 ms with four (each launch ~50 us once
+// several contexts' streams share the hardware queues; profiles/r02/early_quad/).
 #include <algorithm>
 
 #include "kernels.hpp"
 
-#ifndef CIR_ORDER_CUB
-#define CIR_ORDER_CUB 0
-#endif
-
 namespace cir {
 namespace dev {
 
-constexpr int kKeyBits = 16;  // the hipCUB path's key width
 constexpr uint32_t kBins = 4096;
 constexpr unsigned kOrderGrid = 512;  // workgroups of both kernels (at most)
 
@@ -52,12 +44,10 @@ __device__ __forceinline__ uint32_t length_bin(uint32_t k) {
 __global__ __launch_bounds__(256) void k_chain_keys(const uint32_t* __restrict__ len, uint64_t n,
                                                     uint32_t min_lines,
                                                     uint16_t* __restrict__ key,
-                                                    uint32_t* __restrict__ idx,
                                                     uint32_t* __restrict__ count,
                                                     uint32_t* __restrict__ hist) {
   __shared__ uint32_t lh[kBins];
-  if (hist != nullptr)
-    for (uint32_t b = threadIdx.x; b < kBins; b += blockDim.x) lh[b] = 0;
+  for (uint32_t b = threadIdx.x; b < kBins; b += blockDim.x) lh[b] = 0;
   __syncthreads();
   uint32_t nl = 0, mx = 0;
   uint64_t w = 0;
@@ -65,16 +55,9 @@ __global__ __launch_bounds__(256) void k_chain_keys(const uint32_t* __restrict__
        i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t l = len[i];
     const uint32_t k = l == 0 ? 1u : (l >> 7) + ((l & 127u) != 0);  // compressions, <= 2^25
-    if (hist != nullptr) {
-      const uint32_t b = length_bin(k);
-      key[i] = (uint16_t)b;
-      atomicAdd(&lh[b], 1u);
-    } else {
-      // hipCUB path: 16-bit radix key, exact below 32768 lines, then steps
-      // of 1024 lines
-      key[i] = (uint16_t)(k < 32768u ? k : 32768u + ((k - 32768u) >> 10));
-      idx[i] = (uint32_t)i;
-    }
+    const uint32_t b = length_bin(k);
+    key[i] = (uint16_t)b;
+    atomicAdd(&lh[b], 1u);
     if (k >= min_lines)
       ++nl;
     else
@@ -107,9 +90,8 @@ __global__ __launch_bounds__(256) void k_chain_keys(const uint32_t* __restrict__
     if (w) atomicAdd(reinterpret_cast<unsigned long long*>(count + 4), (unsigned long long)w);
     atomicMax(count + 2, mx);
   }
-  if (hist != nullptr)
-    for (uint32_t b = threadIdx.x; b < kBins; b += blockDim.x)
-      if (lh[b]) atomicAdd(&hist[b], lh[b]);
+  for (uint32_t b = threadIdx.x; b < kBins; b += blockDim.x)
+    if (lh[b]) atomicAdd(&hist[b], lh[b]);
 }
 
 // Place chunk c = [c * C, min((c + 1) * C, n)) of the batch into perm in
@@ -166,18 +148,12 @@ __global__ __launch_bounds__(256) void k_order_place(const uint16_t* __restrict_
 
 namespace {
 // scratch: [256 B counters][hist kBins x 4][cursor kBins x 4][key][perm]
-// (the hipCUB path: [key_in][key_out][idx_in][idx_out][temp])
 constexpr uint64_t kHead = 256 + 2ull * kBins * 4;
 }  // namespace
 
 size_t order_scratch_bytes(uint64_t n) {
   const uint64_t arr = (n * 4 + 255) & ~(uint64_t)255;
-  if (!CIR_ORDER_CUB) return kHead + 2 * arr;
-  size_t temp = 0;
-  (void)hipcub::DeviceRadixSort::SortPairsDescending(nullptr, temp, (const uint16_t*)nullptr,
-                                                     (uint16_t*)nullptr, (const uint32_t*)nullptr,
-                                                     (uint32_t*)nullptr, (int)n, 0, kKeyBits);
-  return kHead + ((temp + 255) & ~(size_t)255) + 4 * arr;
+  return kHead + 2 * arr;
 }
 
 hipError_t launch_order_desc(const uint32_t* len, uint64_t n, void* scratch, size_t bytes,
@@ -192,40 +168,21 @@ hipError_t launch_order_desc(const uint32_t* len, uint64_t n, void* scratch, siz
   // gate); count[2] = longest chain; count[4..5] = lane work (k_chain_keys);
   // count[6] = lane tiles claimed (k_lane_rest); then the histogram and the
   // per-bin cursors: one memset for all of them
-  hipError_t e = hipMemsetAsync(count, 0, CIR_ORDER_CUB ? 32 : kHead, s);
+  hipError_t e = hipMemsetAsync(count, 0, kHead, s);
   if (e != hipSuccess) return e;
   *n_long = count;
   const uint64_t kgrid = std::min<uint64_t>((n + 255) / 256, kOrderGrid);
   uint16_t* key = reinterpret_cast<uint16_t*>(p);
-  if (!CIR_ORDER_CUB) {
-    uint32_t* out = reinterpret_cast<uint32_t*>(p + arr);
-    hipLaunchKernelGGL(k_chain_keys, dim3((unsigned)kgrid), dim3(256), 0, s, len, n,
-                       quad_min_lines(n), key, (uint32_t*)nullptr, count, hist);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    const uint64_t chunk = (n + kgrid - 1) / kgrid;
-    hipLaunchKernelGGL(k_order_place, dim3((unsigned)kgrid), dim3(256), 0, s, key, n, chunk,
-                       hist, cursor, out);
-    *perm = out;
-    return hipGetLastError();
-  }
-  uint16_t* key_out = reinterpret_cast<uint16_t*>(p + arr);
-  uint32_t* idx_in = reinterpret_cast<uint32_t*>(p + 2 * arr);
-  uint32_t* idx_out = reinterpret_cast<uint32_t*>(p + 3 * arr);
-  void* temp = p + 4 * arr;
-  size_t temp_bytes = bytes - kHead - 4 * arr;
+  uint32_t* out = reinterpret_cast<uint32_t*>(p + arr);
   hipLaunchKernelGGL(k_chain_keys, dim3((unsigned)kgrid), dim3(256), 0, s, len, n,
-                     quad_min_lines(n), key, idx_in, count, (uint32_t*)nullptr);
+                     quad_min_lines(n), key, count, hist);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  if (n == 1) {  // one chain (hash_bytes, an index footer): nothing to order
-    *perm = idx_in;
-    return hipSuccess;
-  }
-  e = hipcub::DeviceRadixSort::SortPairsDescending(temp, temp_bytes, key, key_out, idx_in,
-                                                   idx_out, (int)n, 0, kKeyBits, s);
-  *perm = idx_out;
-  return e;
+  const uint64_t chunk = (n + kgrid - 1) / kgrid;
+  hipLaunchKernelGGL(k_order_place, dim3((unsigned)kgrid), dim3(256), 0, s, key, n, chunk, hist,
+                     cursor, out);
+  *perm = out;
+  return hipGetLastError();
 }
 
 }  // namespace dev

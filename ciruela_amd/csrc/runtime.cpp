@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <thread>
 
@@ -60,13 +61,11 @@ Device::~Device() {
   if (order_free) (void)hipEventSynchronize(order_free);
   (void)hipFree(order_scratch);
   if (order_free) (void)hipEventDestroy(order_free);
-  if (aux) (void)hipStreamSynchronize(aux);
   if (qstream) (void)hipStreamSynchronize(qstream);
   (void)hipFree(relay_mem);
   if (aux_fork) (void)hipEventDestroy(aux_fork);
   if (aux_join) (void)hipEventDestroy(aux_join);
   if (q_join) (void)hipEventDestroy(q_join);
-  if (aux) (void)hipStreamDestroy(aux);
   if (qstream) (void)hipStreamDestroy(qstream);
   if (single) (void)hipStreamSynchronize(single);
   (void)hipHostFree(single_h);
@@ -75,17 +74,6 @@ Device::~Device() {
   if (single) (void)hipStreamDestroy(single);
   if (compute) (void)hipStreamDestroy(compute);
   if (copy) (void)hipStreamDestroy(copy);
-}
-
-// CIR_ZERO_COPY=1: the staged host paths hand the pinned staging buffers to
-// the hash kernels directly (PCIe reads from the kernels) instead of an SDMA
-// copy into device memory first (A/B: profiles/r02/).
-bool zero_copy() {
-  static const bool on = [] {
-    const char* v = std::getenv("CIR_ZERO_COPY");
-    return v && *v && strcmp(v, "0") != 0;
-  }();
-  return on;
 }
 
 bool trace_enabled() {
@@ -106,18 +94,20 @@ int Device::ensure_slot(Slot& s, uint64_t bytes, uint64_t nblk) {
       CIR_HIP(hipEventCreate(&s.t_hash0));
     }
   }
+  const auto t0 = std::chrono::steady_clock::now();
+  bool grew = false;
   if (bytes > s.cap) {
+    grew = true;
     (void)hipHostFree(s.h_data);
     (void)hipFree(s.d_data);
     s.h_data = nullptr;
     s.d_data = nullptr;
     s.cap = 0;
-    // zero-copy: the kernels read the staging buffer over PCIe, so it must be
-    // coherent (not cached by the GPU between the batches that reuse it)
-    CIR_HIP(hipHostMalloc(&s.h_data, bytes,
-                          zero_copy() ? hipHostMallocMapped | hipHostMallocCoherent
-                                      : hipHostMallocDefault));
-    if (!zero_copy()) CIR_HIP(hipMalloc(&s.d_data, bytes));
+    // (zero-copy staging -- the hash kernels reading the pinned buffer over
+    // PCIe instead of an SDMA copy first -- ran config 5 at 30.0 vs 35.7
+    // GiB/s and config 2 from host memory at 33.7 vs 51.5: profiles/r02/zero_copy/)
+    CIR_HIP(hipHostMalloc(&s.h_data, bytes, hipHostMallocDefault));
+    CIR_HIP(hipMalloc(&s.d_data, bytes));
     s.cap = bytes;
   }
   if (nblk > s.cap_blk) {
@@ -141,46 +131,26 @@ int Device::ensure_slot(Slot& s, uint64_t bytes, uint64_t nblk) {
     CIR_HIP(hipMalloc(&s.d_len, nblk * 4));
     CIR_HIP(hipMalloc(&s.d_out, nblk * 32));
     s.cap_blk = nblk;
+    grew = true;
   }
+  if (grew && trace_enabled())
+    fprintf(stderr, "cir alloc slot %d: %.1f MiB data, %llu blocks in %.2f ms\n",
+            (int)(&s - slot), s.cap / 1048576.0, (unsigned long long)s.cap_blk,
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0)
+                .count());
   return CIR_OK;
 }
 
-// Where the two parts of an ordered batch run (CIR_PART_STREAMS, read when
-// a device first orders a batch; A/B in tools/queue_probe.py,
-// profiles/r02/queue_probe_*.log):
-//   hiq (default): quad part on a non-blocking stream of the greatest
-//        priority, lane part on the caller's stream.  HIP pools hardware
-//        queues per priority, so the quad part never shares a queue with the
-//        caller's (or any other normal-priority) stream, and its workgroups
-//        are dispatched first;
-//   own2: both parts on CU-masked streams (a hardware queue each; these are
-//        blocking streams, so they synchronise with the null stream);
-//   plain: quad part on the caller's stream, lane part on a plain stream
-//        (round 1: the two serialised whenever they shared a queue).
-enum PartMode { kPartHiq = 0, kPartOwn2 = 1, kPartPlain = 2 };
-static int part_mode() {
-  const char* v = std::getenv("CIR_PART_STREAMS");
-  if (v && strcmp(v, "own2") == 0) return kPartOwn2;
-  if (v && strcmp(v, "plain") == 0) return kPartPlain;
-  return kPartHiq;
-}
-
-static hipError_t create_cu_masked_stream(int dev_id, hipStream_t* s) {
-  hipDeviceProp_t prop;
-  hipError_t e = hipGetDeviceProperties(&prop, dev_id);
-  if (e != hipSuccess) return e;
-  std::vector<uint32_t> mask((prop.multiProcessorCount + 31) / 32, 0u);
-  for (int c = 0; c < prop.multiProcessorCount; ++c) mask[c / 32] |= 1u << (c % 32);
-  return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
-}
-
+// The two parts of an ordered batch: the quad part on a non-blocking stream
+// of the greatest priority, the lane part on the caller's stream.  HIP pools
+// hardware queues per priority, so the quad part never shares a queue with
+// the caller's (or any other normal-priority) stream, and its workgroups are
+// dispatched first.  Measured against the alternatives (round 2,
+// profiles/r02/queue_probe_*.log: config 3 at 1 / 4 contexts per process):
+// plain streams 866 / 616 GiB/s (the parts serialised whenever they shared a
+// hardware queue), both parts on CU-masked streams 840 / 768, this 867 / 758
+// (830 after the gate and the counting sort).
 static hipError_t create_part_streams(Device& d) {
-  d.part_mode = part_mode();
-  if (d.part_mode == kPartOwn2) {
-    hipError_t e = create_cu_masked_stream(d.id, &d.qstream);
-    return e != hipSuccess ? e : create_cu_masked_stream(d.id, &d.aux);
-  }
-  if (d.part_mode == kPartPlain) return hipStreamCreateWithFlags(&d.aux, hipStreamNonBlocking);
   int least = 0, greatest = 0;
   hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
   if (e != hipSuccess) return e;
@@ -234,11 +204,11 @@ Device* stream_device(cir_ctx* ctx, hipStream_t s) {
 bool valid_hash_type(int ht) { return ht == CIR_HASH_BLAKE2B_256 || ht == CIR_HASH_SHA512_256; }
 
 int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, const uint32_t* len,
-                      uint64_t n, uint8_t* out, hipStream_t s, int ht) {
+                      uint64_t n, uint8_t* out, hipStream_t s, int ht, bool warm_only) {
   // Every batch is ordered (even a single chain: an index footer is one long
   // chain and runs in quad mode).
   if (n == 0) return CIR_OK;
-  if (n > (uint64_t)INT32_MAX)  // hipCUB's item count is an int (order.hip)
+  if (n > (uint64_t)INT32_MAX)  // 32-bit chain indices in the order (order.hip)
     return fail(CIR_EINVAL, "more than 2^31-1 descriptors in one ordered batch");
   std::lock_guard<std::mutex> lk(d.order_mu);
   // Streams, events and the ordering scratch live on d's device, whatever
@@ -256,6 +226,8 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
     CIR_HIP(hipMalloc(&d.order_scratch, need));
     d.order_cap = need;
   }
+  // cir_init's warm-up: the scratch sized for n descriptors, one hashed
+  if (warm_only) n = 1;
   CIR_HIP(hipStreamWaitEvent(s, d.order_free, 0));
   // diagnostics: a fresh event set per batch while timing is on (at most
   // kMaxTimedBatches per enable)
@@ -278,7 +250,7 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
     CIR_HIP(dev::launch_sha_desc(arena, off, len, perm, n, out, s));
   else
     CIR_HIP(dev::launch_mixed(arena, off, len, perm, n_long, n, out, s, d.qstream ? d.qstream : s,
-                              d.aux ? d.aux : s, d.aux_fork, d.q_join, d.aux_join,
+                              s, d.aux_fork, d.q_join, d.aux_join,
                               d.relay_mem ? &d.relay : nullptr, tev ? tev + 2 : nullptr));
   CIR_HIP(hipEventRecord(d.order_free, s));
   return CIR_OK;
@@ -290,10 +262,8 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
 static int slot_submit_impl(Device& d, Slot& s, uint64_t bytes, uint64_t nblk,
                             uint64_t chunk_bs, int ht) {
   if (s.t_copy0) CIR_HIP(hipEventRecord(s.t_copy0, d.copy));
-  // zero-copy: the hash kernels read the pinned slot over PCIe themselves
-  const uint8_t* src = zero_copy() ? s.h_data : s.d_data;
-  if (!zero_copy())
-    CIR_HIP(hipMemcpyAsync(s.d_data, s.h_data, bytes, hipMemcpyHostToDevice, d.copy));
+  const uint8_t* src = s.d_data;
+  CIR_HIP(hipMemcpyAsync(s.d_data, s.h_data, bytes, hipMemcpyHostToDevice, d.copy));
   if (chunk_bs == 0) {
     CIR_HIP(hipMemcpyAsync(s.d_off, s.h_off, nblk * 8, hipMemcpyHostToDevice, d.copy));
     CIR_HIP(hipMemcpyAsync(s.d_len, s.h_len, nblk * 4, hipMemcpyHostToDevice, d.copy));
@@ -587,18 +557,48 @@ static int export_hashes(const std::vector<uint8_t>& h, uint8_t** out, size_t* n
   return CIR_OK;
 }
 
-// Everything a device state needs that does not depend on a call's sizes,
-// created here so the asynchronous *_dev entry points never allocate or
-// synchronise: the staging and part streams, their events and the relay
-// scratch (zeroed with one synchronised memset).  Caller holds a DeviceGuard.
-static int init_device(Device& d) {
+// Everything a device state needs, created here rather than by the first
+// call that uses it: the asynchronous *_dev entry points then never allocate
+// or synchronise, and the first scan / host batch of a process runs as fast
+// as the later ones (round 3: the staging slots' allocation and the first
+// kernel launches were ~0.1 s of config 5's first scan).
+//   * the staging, part and footer-chain streams, their events and the relay
+//     scratch (zeroed with one synchronised memset);
+//   * the three staging slots at the context's staging size (pinned host +
+//     device buffers, descriptor and digest buffers for a full batch) and
+//     the ordering scratch for one such batch;
+//   * one tiny chunk-form hash and one ordered descriptor batch on the
+//     compute stream, which load the code object and touch every buffer.
+// Caller holds a DeviceGuard.
+static int init_device(Device& d, uint64_t staging) {
   CIR_HIP(hipSetDevice(d.id));
   CIR_HIP(hipStreamCreateWithFlags(&d.compute, hipStreamNonBlocking));
   CIR_HIP(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
-  std::lock_guard<std::mutex> lk(d.order_mu);
-  int rc = ensure_part_streams(d);
-  if (rc == CIR_OK) rc = ensure_relay(d);
-  return rc;
+  CIR_HIP(hipStreamCreateWithFlags(&d.chain, hipStreamNonBlocking));
+  CIR_HIP(hipMalloc(&d.chain_state, 16 * 8));
+  for (int b = 0; b < 2; ++b)
+    CIR_HIP(hipEventCreateWithFlags(&d.chain_done[b], hipEventDisableTiming));
+  {
+    std::lock_guard<std::mutex> lk(d.order_mu);
+    int rc = ensure_part_streams(d);
+    if (rc == CIR_OK) rc = ensure_relay(d);
+    if (rc) return rc;
+  }
+  const uint64_t cap_blk = std::max<uint64_t>(staging / 512, 4096);
+  for (Slot& s : d.slot) {
+    const int rc = d.ensure_slot(s, std::max<uint64_t>(staging, 16), cap_blk);
+    if (rc) return rc;
+  }
+  Slot& s = d.slot[0];
+  CIR_HIP(hipMemsetAsync(s.d_data, 0, 4096, d.compute));
+  CIR_HIP(hipMemsetAsync(s.d_off, 0, 8, d.compute));
+  CIR_HIP(hipMemsetAsync(s.d_len, 0, 4, d.compute));
+  CIR_HIP(dev::launch_chunks(s.d_data, 4096, 1024, s.d_out, d.compute));
+  const int rc = hash_desc_ordered(d, s.d_data, s.d_off, s.d_len, cap_blk, s.d_out, d.compute,
+                                   CIR_HASH_BLAKE2B_256, /*warm_only=*/true);
+  if (rc) return rc;
+  CIR_HIP(hipStreamSynchronize(d.compute));
+  return CIR_OK;
 }
 
 // Process-default context for cir_blake2b256 (BlockHash::hash_bytes has no
@@ -646,7 +646,7 @@ int cir_init(cir_ctx** out, uint32_t device_mask, uint64_t staging_bytes) {
     if (rc) return rc;
     auto d = std::make_unique<Device>();
     d->id = i;
-    rc = init_device(*d);
+    rc = init_device(*d, ctx->staging);
     if (rc) return rc;
     ctx->devs.push_back(std::move(d));
   }
@@ -661,7 +661,7 @@ int cir_init(cir_ctx** out, uint32_t device_mask, uint64_t staging_bytes) {
       for (size_t i = 0; i < n0; ++i) {
         auto d = std::make_unique<Device>();
         d->id = ctx->devs[i]->id;
-        const int rc = init_device(*d);
+        const int rc = init_device(*d, ctx->staging);
         if (rc) return rc;
         ctx->devs.push_back(std::move(d));
       }
@@ -731,8 +731,8 @@ int cir_hash_blocks_dev_ht(cir_ctx* ctx, int hash_type, const void* d_arena,
     return fail(CIR_EINVAL, "null device pointer");
   if (reinterpret_cast<uintptr_t>(d_out) & 15u)
     return fail(CIR_EINVAL, "d_out must be 16-byte aligned");
-  // descriptor indices are 32-bit in the kernels and the ordering sorts an
-  // int-sized item count (hipCUB): one call takes at most 2^31-1 blocks
+  // descriptor indices are 32-bit in the kernels and in the ordering's
+  // permutation: one call takes at most 2^31-1 blocks
   if (nblk > (size_t)INT32_MAX) return fail(CIR_EINVAL, "more than 2^31-1 descriptors");
   hipStream_t s = (hipStream_t)stream;
   // Context-less calls hash in descriptor order, one lane per chain; with a
@@ -842,7 +842,7 @@ static int single_shot(int ht, const uint8_t* p, size_t n, uint8_t* out) {
   cir_ctx* ctx = nullptr;
   int rc = default_ctx(&ctx);
   if (rc) return rc;
-  if (ht == CIR_HASH_BLAKE2B_256 && n <= kSingleMax && !std::getenv("CIR_SINGLE_STAGED"))
+  if (ht == CIR_HASH_BLAKE2B_256 && n <= kSingleMax)
     return single_launch(*ctx->devs[0], p, n, out);
   static const uint8_t empty = 0;
   const uint64_t off = 0;

@@ -67,8 +67,6 @@ struct Slot {
 
 // CIR_TRACE set to a non-empty value other than "0": per-batch timings on stderr.
 bool trace_enabled();
-// CIR_ZERO_COPY: hash kernels read the pinned staging slots directly.
-bool zero_copy();
 
 struct Device {
   int id = 0;
@@ -87,10 +85,8 @@ struct Device {
   hipEvent_t order_free = nullptr;
   // An ordered batch runs its quad part on `qstream` (a high-priority
   // stream: a hardware queue of its own) and its lane part on the caller's
-  // stream, forked and joined with events (runtime.cpp part_mode; a null
-  // qstream / aux means the caller's stream).
-  int part_mode = 0;
-  hipStream_t aux = nullptr, qstream = nullptr;
+  // stream, forked and joined with events (runtime.cpp create_part_streams).
+  hipStream_t qstream = nullptr;
   hipEvent_t aux_fork = nullptr, aux_join = nullptr, q_join = nullptr;
   // relayed quad chains (used on qstream only; allocated at full capacity
   // by cir_init)
@@ -128,7 +124,8 @@ struct Device {
 // asynchronously, wait() returns the digests in h_out.
 int slot_submit(Device& d, Slot& s, uint64_t bytes, uint64_t nblk, int ht = CIR_HASH_BLAKE2B_256);
 int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, const uint32_t* len,
-                      uint64_t n, uint8_t* out, hipStream_t s, int ht = CIR_HASH_BLAKE2B_256);
+                      uint64_t n, uint8_t* out, hipStream_t s, int ht = CIR_HASH_BLAKE2B_256,
+                      bool warm_only = false);
 bool valid_hash_type(int ht);
 int slot_wait(Device& d, Slot& s);
 

@@ -367,6 +367,7 @@ struct FooterChain {
       const bool last = final && piece == n;
       CIR_HIP(hipEventSynchronize(d.chain_done[k]));  // buffer k free again
       if (piece > d.chain_cap[k]) {
+        const double ta = trace_on() ? now_ms() : 0;
         (void)hipHostFree(d.chain_h[k]);
         (void)hipFree(d.chain_d[k]);
         d.chain_h[k] = nullptr;
@@ -376,6 +377,9 @@ struct FooterChain {
         CIR_HIP(hipHostMalloc(&d.chain_h[k], cap, hipHostMallocDefault));
         CIR_HIP(hipMalloc(&d.chain_d[k], cap));
         d.chain_cap[k] = cap;
+        if (trace_on())
+          fprintf(stderr, "cir_scan footer buffer %d: %.1f MiB in %.2f ms\n", k,
+                  cap / 1048576.0, now_ms() - ta);
       }
       if (piece) {
         memcpy(d.chain_h[k], body.data() + fed, piece);
@@ -554,7 +558,9 @@ int cir_index_rewrite(cir_ctx* ctx, const uint8_t* in, size_t len, uint8_t** out
   // parsed before the context is needed: a malformed index is a ParseError
   // whatever the device state (RawIndex::into_mut, src/cluster/download.rs:175-181)
   if (!dirsig::parse(in, len, &idx, &err)) return fail(CIR_EPARSE, "ParseError: " + err);
-  if (!ctx) return fail(CIR_EINVAL, "null ctx");
+  // fill_dirs (src/cluster/download.rs:108-167) on the host, also before the
+  // context is needed: a file and a directory of one name is a PathConflict
+  // (:138-140), whatever the device state
   Tree root;
   Tree* cur = &root;
   std::vector<std::string> parts;
@@ -582,6 +588,7 @@ int cir_index_rewrite(cir_ctx* ctx, const uint8_t* in, size_t len, uint8_t** out
     it.target = std::move(e.target);
     (*cur)[parts.back()] = std::move(it);
   }
+  if (!ctx) return fail(CIR_EINVAL, "null ctx");
   dirsig::Emitter em(idx.header);
   emit_tree(em, "/", root);
   const std::string& body = em.body();

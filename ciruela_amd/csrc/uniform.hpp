@@ -11,10 +11,9 @@ namespace dev {
 constexpr int kWaves = kThreads / 64;
 
 // cache-policy bits of the LDS-DMA loads: 2 = nt (streamed, read once;
-// MI355X_MICROARCH.md nt-weights).  A/B in-process: within 1 % of 0.
-#ifndef CIR_DMA_AUX
-#define CIR_DMA_AUX 2
-#endif
+// MI355X_MICROARCH.md nt-weights).  A/B in-process: within 1 % of 0
+// (profiles/r01/ablib_nt_occ.log).
+constexpr int kDmaAux = 2;
 
 // ---------------------------------------------------------------------------
 // LDS image of one wave's message lines (8 KiB, no padding).
@@ -31,7 +30,7 @@ constexpr int kWaveLds = 8192;
 
 // One wave hashes the 64 equal blocks starting at wsrc (bs bytes each,
 // `lines` = bs / 128 message lines) into out[0 .. 64*32).
-// Register budget: <= 96 VGPRs (5 waves per SIMD, 5 x 32 KiB LDS per CU).
+// Register budget: k_chunks runs it at 4 waves per SIMD (107 VGPRs, no spills).
 // The per-lane DMA offsets and LDS read addresses are recomputed every line
 // from one register each (one full-rate v_xor_b32 apiece) instead of being
 // hoisted into 16 + 8 registers; the DMA base address stays scalar.
@@ -68,7 +67,7 @@ __device__ __forceinline__ void uniform_glds_wave(const uint8_t* __restrict__ ws
       }
       __builtin_amdgcn_global_load_lds(
           (const void __attribute__((address_space(1)))*)src,
-          (void __attribute__((address_space(3)))*)(wl + j * 1024), 16, 0, CIR_DMA_AUX);
+          (void __attribute__((address_space(3)))*)(wl + j * 1024), 16, 0, kDmaAux);
     }
   };
 

@@ -199,6 +199,38 @@ def test_invalid_paths_rejected(tmp_path, bad):
     assert len(r) == 0
 
 
+PATH_CONFLICT_INDEXES = [
+    # a file, then a directory line through the same name (download.rs:138-140)
+    b"DIRSIGNATURE.v1 blake2b/256 block_size=4096\n/\n  a f 0\n/a\n  b f 0\n",
+    # a deeper directory line crossing a file of an earlier directory
+    b"DIRSIGNATURE.v1 sha512/256 block_size=4096\n/\n/d\n  x f 0\n/d/x/y\n  z f 0\n",
+    # a symlink is not a directory either
+    b"DIRSIGNATURE.v1 blake2b/256 block_size=4096\n/\n  l s /tmp\n/l\n  f f 0\n",
+]
+
+
+@pytest.mark.parametrize("bad", PATH_CONFLICT_INDEXES)
+def test_rewrite_path_conflict(bad):
+    """IndexParseEnum::PathConflict (fill_dirs, src/cluster/download.rs:
+    126-140): a directory line whose path runs through a file or a symlink
+    of an earlier line.  RawIndex::into_mut fails with it, so the rewrite
+    (cir_index_rewrite) returns CIR_EPARSE naming the path -- detected while
+    the tree is rebuilt on the host, before any device is needed."""
+    import ctypes
+    idx = bad + b"ab" * 32 + b"\n"
+    out, ln = ctypes.c_void_p(), ctypes.c_size_t()
+    rc = _native.lib.cir_index_rewrite(None, idx, len(idx), ctypes.byref(out), ctypes.byref(ln))
+    assert rc == _native.CIR_EPARSE
+    assert b"conflicts with others" in _native.lib.cir_last_error()
+    # the same tree without the conflicting line passes fill_dirs and stops
+    # only at the missing context (the footer is hashed on the GPU)
+    ok = b"\n".join(ln_ for ln_ in bad.split(b"\n")
+                    if not (ln_.startswith(b"/") and ln_ != b"/" and (
+                        ln_ in (b"/a", b"/l", b"/d/x/y")))) + b"ab" * 32 + b"\n"
+    rc = _native.lib.cir_index_rewrite(None, ok, len(ok), ctypes.byref(out), ctypes.byref(ln))
+    assert rc == _native.CIR_EINVAL and b"null ctx" in _native.lib.cir_last_error()
+
+
 def test_valid_odd_names_still_parse(tmp_path):
     """Names that merely look like paths stay valid: `...`, `.x`, escaped bytes."""
     idx = (b"DIRSIGNATURE.v1 blake2b/256 block_size=4096\n/\n  ... f 0\n  .x f 0\n"
@@ -208,7 +240,7 @@ def test_valid_odd_names_still_parse(tmp_path):
 
 def test_descriptor_count_limit():
     """cir_hash_blocks_dev_ht takes at most 2^31-1 descriptors (32-bit block
-    indices in the kernels, an int item count in the hipCUB sort): larger
+    indices in the kernels and in the ordering's permutation): larger
     batches are rejected before anything touches a device."""
     lib = _native.lib
     for n in (1 << 31, (1 << 32) + 5):

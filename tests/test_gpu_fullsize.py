@@ -9,6 +9,7 @@ Config 2 (1 M x 32 KiB = 32 GiB) and config 3 (10 GiB of mixed 4 KiB /
   * determinism: a second launch gives the identical digest array, and the
     per-lane direct loader gives the same array as the LDS-DMA loader.
 """
+import ctypes
 import os
 import random
 from concurrent.futures import ThreadPoolExecutor
@@ -234,5 +235,94 @@ def test_scan_tree_above_2gib(gpu, oracle, tmp_path):
         want = cpu_indexer.index(top, 32768, THREADS)
         assert got == want
         assert gpu.get_hash(got) == bytes.fromhex(want.rstrip(b"\n").split(b"\n")[-1].decode())
+    finally:
+        shutil.rmtree(top, ignore_errors=True)
+
+
+def test_config1_cli_sync_append(gpu, tmp_path):
+    """Config 1 at its stated size (BASELINE.json configs[0]):
+    the 100-file / 10 MiB tree of 10 subdirectories that bench.py builds
+    (make_config1_tree, default_rng(1)), indexed by one `ciruela-index sync
+    --append SRC:/bench` process (the indexing half of `ciruela sync`,
+    src/client/sync/uploads.rs:49-59, 4 disk threads).  The .ds1 it writes
+    equals the scan oracle's index byte for byte, its name and the printed
+    image id are the footer hash, and every block hash in it equals
+    hash_bytes(block) (src/daemon/tracking/fetch_blocks.rs:77)."""
+    import subprocess
+    import sys
+    from conftest import ROOT, oracle_digest
+    import dirsig_oracle
+    sys.path.insert(0, ROOT)
+    import bench
+    src = tmp_path / "tree"
+    total = bench.make_config1_tree(str(src))
+    assert total == 10 << 20
+    assert sum(len(fs) for _, _, fs in os.walk(src)) == 100
+    idx_dir = tmp_path / "idx"
+    idx_dir.mkdir()
+    out = subprocess.check_output([os.path.join(ROOT, "bin", "ciruela-index"), "sync",
+                                   "--index-dir", str(idx_dir), "--append", "%s:/bench" % src],
+                                  timeout=120)
+    image_id, kind, dest, srcp = out.decode().split()
+    assert (kind, dest, srcp) == ("append", "/bench", str(src))
+    written = (idx_dir / (image_id + ".ds1")).read_bytes()
+    want = dirsig_oracle.scan(str(src))
+    assert written == want
+    assert want.rstrip(b"\n").split(b"\n")[-1].decode() == image_id
+    assert gpu.get_hash(written).hex() == image_id
+    # per-block invariant on a sample of files, through the oracle's own hash
+    oracle = bench.load_oracle()
+    oracle.oracle_blake2b256.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    checked = 0
+    for line in written.split(b"\n"):
+        parts = line.split()
+        if len(parts) >= 4 and parts[1] == b"f" and line.startswith(b"  "):
+            name, size, hashes = parts[0].decode(), int(parts[2]), parts[3:]
+            path = next(os.path.join(dp, name) for dp, _, fs in os.walk(src) if name in fs)
+            blob = open(path, "rb").read()
+            assert len(blob) == size and len(hashes) == (size + 32767) // 32768
+            for k in (0, len(hashes) - 1):
+                assert oracle_digest(oracle, blob[32768 * k:32768 * (k + 1)]).hex() == \
+                    hashes[k].decode()
+            checked += 1
+    assert checked == 100
+
+
+def test_config5_full_tree(gpu):
+    """Config 5 at its stated size (BASELINE.json configs[4]): the 50 GiB
+    tmpfs tree bench.py indexes (make_tree: 1600 files x 32 MiB in 40
+    directories), scanned once through cir_scan_v1 with the default staging
+    (3 x 256 MiB pinned slots) in a fresh context, and the index checked byte
+    for byte against the CPU indexer restatement (oracle/cpu_indexer.py:
+    every block by the threaded C oracle, emitter and footer by
+    dirsig_oracle).  Skipped when /dev/shm cannot hold the tree."""
+    import shutil
+    import sys
+    import tempfile
+    from conftest import ROOT
+    import cpu_indexer
+    sys.path.insert(0, ROOT)
+    import bench
+    if not os.path.isdir("/dev/shm"):
+        pytest.skip("no /dev/shm")
+    st = os.statvfs("/dev/shm")
+    if st.f_bavail * st.f_frsize < (55 << 30):
+        pytest.skip("/dev/shm has %.1f GiB free, config 5 needs 55"
+                    % (st.f_bavail * st.f_frsize / (1 << 30)))
+    top = tempfile.mkdtemp(prefix="cir_cfg5_", dir="/dev/shm")
+    try:
+        nfiles = bench.make_tree(top, 50.0)
+        assert nfiles == 1600
+        ctx = gpu.Context(device_mask=1)
+        cfg = gpu.ScannerConfig.new().threads(16).add_dir(top, "/")
+        got = gpu.v1.scan(cfg, context=ctx)
+        want = cpu_indexer.index(top, 32768, THREADS)
+        assert len(got) == len(want)
+        assert got == want
+        ndirs = sum(len(ds) for _, ds, _ in os.walk(top))
+        nfiles = sum(len(fs) for _, _, fs in os.walk(top))
+        assert ndirs == 40 and nfiles >= 1600
+        # header, "/", one line per directory and per file, footer
+        assert got.count(b"\n") == 3 + ndirs + nfiles
     finally:
         shutil.rmtree(top, ignore_errors=True)

@@ -98,6 +98,20 @@ for s in "$@"; do
         -d gpurun_out/prof3 -o run -- python3 bench.py --workload config3 --steps 3 --warmup 1 \
         > gpurun_out/prof3.log 2>&1
       cat gpurun_out/prof3/run_kernel_stats.csv | cut -c1-200 ;;
+    pmc3)  # SQ counters of config 3 per dispatch (k_quad_long's per-compression budget)
+      i=0
+      for c in "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES" \
+               "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_INSTS_SMEM" \
+               "SQ_WAIT_ANY SQ_INSTS_BRANCH SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_ANY"; do
+        i=$((i+1))
+        step "pmc3_$i" 300 rocprofv3 --pmc $c --output-format csv \
+          -d "gpurun_out/pmc3_$i" -o run -- python3 bench.py --workload config3 --steps 2 \
+          --warmup 1 > "gpurun_out/pmc3_$i.log" 2>&1
+      done ;;
+    firstread)
+      step firstread 600 python tools/first_read_probe.py --gib "${TREE_GIB:-16}" \
+        --read-first "${READ_FIRST:-1}" > gpurun_out/firstread.log 2>&1
+      cat gpurun_out/firstread.log ;;
     cfg3ab)
       for lib in abtest/*.so; do
         CIRUELA_AMD_LIB=$PWD/$lib step "cfg3_$lib" 300 python bench.py --workload config3 --steps 5 --warmup 1 \

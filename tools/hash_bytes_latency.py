@@ -1,6 +1,7 @@
 """Latency of BlockHash::hash_bytes (cir_blake2b256, host buffer in, digest
-out) per call, the one-launch path (k_single) against the staged batch path
-(CIR_SINGLE_STAGED=1), each checked against hashlib.
+out) per call through the one-launch path (k_single), checked against
+hashlib.  (Round 2 also timed the staged batch path here: 77-88 / 119-128 /
+401-421 us at 0 B / 4 KiB / 32 KiB, profiles/r02_final/latency.log.)
 
     python tools/hash_bytes_latency.py [--calls 100]
 """
@@ -18,11 +19,7 @@ def main():
     ap.add_argument("--calls", type=int, default=100)
     args = ap.parse_args()
     import ciruela_amd as ca
-    for mode in ("single", "staged"):
-        if mode == "staged":
-            os.environ["CIR_SINGLE_STAGED"] = "1"
-        else:
-            os.environ.pop("CIR_SINGLE_STAGED", None)
+    for mode in ("single",):
         for n in (0, 100, 4096, 32768, 1 << 20):
             data = os.urandom(n)
             want = hashlib.blake2b(data, digest_size=32).digest()

@@ -1,8 +1,8 @@
 """Shape sweep of cir_hash_chunks_dev (one device-resident file, context
 path): GiB/s per (block size, block count), one process, HIP events on the
-launch stream.  Run once with CIR_RELAY=0 and once without to A/B the relay
-(k_quad_relay); every shape's digests are compared between the two runs via
-a checksum column.  SWEEP_DESC=1: the same blocks as a descriptor batch
+launch stream; a checksum column per shape compares the digests between
+runs of two builds (the relay's A/B in round 2 used an environment switch
+that no longer exists: build the variant instead, tools/build_variant.sh).  SWEEP_DESC=1: the same blocks as a descriptor batch
 (cir_hash_blocks_dev).  Diagnostics only (DESIGN.md §5 shapes)."""
 import hashlib
 import os
@@ -43,7 +43,7 @@ def main():
     data = torch.empty(maxb, dtype=torch.uint8, device=dev)
     ca._n.check(ca._n.lib.cir_fill_splitmix64_dev(data.data_ptr(), maxb, 0x5EED, 0, 0, stream))
     out = torch.empty(max(n for _, n in SHAPES) * 32, dtype=torch.uint8, device=dev)
-    relay = os.environ.get("CIR_RELAY", "1")
+    relay = "1"
     desc = os.environ.get("SWEEP_DESC") == "1"  # the same blocks as descriptors
     for bs, n in SHAPES:
         nbytes = bs * n

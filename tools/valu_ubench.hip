@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "blake2b_dev.hpp"
+#include "blake2b_variants.hpp"
 #include "uniform.hpp"
 
 #define CHECK(x)                                                              \
