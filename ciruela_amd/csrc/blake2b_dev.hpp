@@ -406,13 +406,32 @@ constexpr int kQuadFromPrev = 0x93;   // lane i <- lane i+3  (quad_perm [3,0,1,2
 #define CIR_QR(K0, K1, K2, K3)                                                \
   CIR_QG_DPP(CIR_QP_93, CIR_QP_4E, CIR_QP_39, CIR_M(K0), CIR_M(K1))           \
   CIR_QG_DPP(CIR_QP_39, CIR_QP_4E, CIR_QP_93, CIR_M(K2), CIR_M(K3))
-#define CIR_QCOMPRESS                                                         \
-  CIR_QG_PLAIN(CIR_M(0), CIR_M(1))                                            \
+// column step of round 0 straight from the chain value and the constants
+// (the hand-scheduled loop): a = h0 (v[52:53]), b = h1 (v[54:55]), c = cv,
+// d = (v46, dh) are read where they are instead of being copied into
+// v[40:47] first (4 moves fewer per compression); the step writes a, b, c,
+// d into v[40:47] as CIR_QG_PLAIN does.  Its first xor is the 8-byte VOP3
+// encoding: CIR_QFAST's lone 4-byte s_waitcnt ahead of it would otherwise
+// leave every later DPP instruction straddling an 8-byte boundary (~10 %
+// slower for a wave alone, see CIR_QALIGN; a config-3 run without it lost
+// 10 % of the quad part, profiles/r03/).
+#define CIR_QG_PLAIN_H(X, Y)                                                  \
+  "v_lshl_add_u64 v[40:41], v[52:53], 0, " X "\n"                             \
+  "v_lshl_add_u64 v[40:41], v[40:41], 0, v[54:55]\n"                          \
+  "v_xor_b32_e64 v48, %[dh], v41\n"                                           \
+  "v_xor_b32 v49, v46, v40\n"                                                 \
+  "v_lshl_add_u64 v[44:45], %[cv], 0, v[48:49]\n"                             \
+  "v_xor_b32 v50, v54, v44\n"                                                 \
+  "v_xor_b32 v51, v55, v45\n"                                                 \
+  "v_alignbit_b32 v42, v51, v50, 24\n"                                        \
+  "v_alignbit_b32 v43, v50, v51, 24\n" CIR_QG_TAIL(Y)
+#define CIR_QCOMPRESS_REST                                                    \
   CIR_QG_DPP(CIR_QP_39, CIR_QP_4E, CIR_QP_93, CIR_M(2), CIR_M(3))             \
   CIR_QR(4, 5, 6, 7) CIR_QR(8, 9, 10, 11) CIR_QR(12, 13, 14, 15)              \
   CIR_QR(16, 17, 18, 19) CIR_QR(20, 21, 22, 23) CIR_QR(24, 25, 26, 27)        \
   CIR_QR(28, 29, 30, 31) CIR_QR(32, 33, 34, 35) CIR_QR(36, 37, 38, 39)        \
   CIR_QR(0, 1, 2, 3) CIR_QR(4, 5, 6, 7) "s_nop 1\n"
+#define CIR_QCOMPRESS CIR_QG_PLAIN(CIR_M(0), CIR_M(1)) CIR_QCOMPRESS_REST
 #define CIR_MO(k) [m##k] "v"(m[k])
 
 __device__ __forceinline__ void compress_quad_asm(uint64_t& a, uint64_t& b, uint64_t& c,
@@ -458,16 +477,13 @@ __device__ __forceinline__ void compress_quad_asm(uint64_t& a, uint64_t& b, uint
 #define CIR_QFAST                                                             \
   CIR_QALIGN                                                                  \
   "v_bitop3_b32 v46, %[dl], %[t], %[lm] bitop3:0x78\n"                        \
-  "v_mov_b32 v47, %[dh]\n"                                                    \
   "s_waitcnt vmcnt(2)\n"                                                      \
-  "v_mov_b64 v[40:41], v[52:53]\n"                                            \
-  "v_mov_b64 v[42:43], v[54:55]\n"                                            \
-  "v_mov_b64_e64 v[44:45], %[cv]\n"                                           \
   "ds_write_b128 %[wr], %[u]\n"                                               \
   "ds_write_b128 %[wr], %[w] offset:16\n"                                     \
   "global_load_dwordx4 %[u], %[ptr], off\n"                                   \
   "global_load_dwordx4 %[w], %[ptr], off offset:16\n"                         \
-  "v_lshl_add_u64 %[ptr], %[ptr], 0, %[step]\n" CIR_RD40 CIR_QCOMPRESS        \
+  "v_lshl_add_u64 %[ptr], %[ptr], 0, %[step]\n" CIR_RD40                      \
+  CIR_QG_PLAIN_H(CIR_M(0), CIR_M(1)) CIR_QCOMPRESS_REST                       \
   "v_xor_b32_dpp v48, v44, v40" CIR_QP_4E "\n"                                \
   "v_xor_b32_dpp v49, v45, v41" CIR_QP_4E "\n"                                \
   "v_xor_b32_dpp v54, v42, v54" CIR_QP_93 "\n"                                \

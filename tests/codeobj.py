@@ -45,8 +45,9 @@ def gfx950_objects(tmpdir, lib=LIB):
     return objs
 
 
-def disassembly(tmpdir):
-    """{mangled kernel name: [instruction text without comments]}."""
+def disassembly(tmpdir, with_addr=False):
+    """{mangled kernel name: [instruction text without comments]}, or
+    [(address, text)] with with_addr."""
     out = {}
     for obj in gfx950_objects(tmpdir):
         asm = subprocess.check_output([os.path.join(LLVM, "llvm-objdump"), "-d",
@@ -61,7 +62,11 @@ def disassembly(tmpdir):
                 continue
             ins = line.split("//")[0].strip()
             if name and ins:
-                body.append(ins)
+                if with_addr:
+                    m = re.search(r"//\s*([0-9A-Fa-f]+):", line)
+                    body.append((int(m.group(1), 16) if m else None, ins))
+                else:
+                    body.append(ins)
         if name:
             out[name] = body
     return out

@@ -59,3 +59,25 @@ def test_known_spills_stay_bounded(res):
     (sha,) = one(res, "k_sha_desc").values()
     assert sha["vgpr_count"] <= 102 and sha["vgpr_spill_count"] == 0
     assert sha["sgpr_spill_count"] <= 2
+
+
+@pytest.mark.parametrize("short", ["k_quad_long", "k_quad_chunks", "k_quad_relay",
+                                   "k_desc_relay", "k_chain_step", "k_single"])
+def test_quad_dpp_instructions_are_8_byte_aligned(tmp_path, short):
+    """A VOP2 DPP instruction (8 bytes) that straddles an 8-byte boundary
+    issues ~10 % slower for a wave alone (tools/align_ubench.hip), and the
+    quad kernels moved 7-10 % with nothing but their code offset
+    (profiles/r02/quad_fast/ab_fastpad.log): every quad asm block starts
+    with .p2align 3 and keeps its 4-byte instructions in pairs
+    (blake2b_dev.hpp CIR_QALIGN).  Checked on the built code object."""
+    table = codeobj.disassembly(str(tmp_path), with_addr=True)
+    hits = codeobj.find(table, short)
+    assert hits, short
+    for name, body in hits.items():
+        # the DPP carry pairs come only from the asm G steps; the compiler's
+        # own DPP xors (the general path's finalisation) are not aligned by it
+        dpp = [(a, ins) for a, ins in body if ins.split()[0] in ("v_add_co_u32_dpp",
+                                                                  "v_addc_co_u32_dpp")]
+        assert dpp, name
+        bad = [(hex(a), ins) for a, ins in dpp if a is None or a % 8]
+        assert not bad, (name, len(bad), len(dpp), bad[:3])
