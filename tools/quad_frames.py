@@ -13,9 +13,9 @@ different G indices reads one of them across lanes by DPP:
     two message adds of a step (a + x, a + y) fill one slot each for free.
 For every 2-step periodic assignment this prints the Pareto set of
 (costly adds, fillers) per 2 steps.  Result: (4, 0) -- what the loop does --
-or (3, 7) / (2, 9), against ~7.5 independent instructions per 2 steps that
-could fill (the 45 loads / reads / writes of a compression): a gain of at
-most ~12 of 588 instructions per compression.
+or (3, 7) / (2, 9), against ~3.75 independent instructions per 2 steps that
+could fill (the 45 loads / reads / writes of a compression over its 12 step
+pairs): the missing fillers would be s_nops, so (4, 0) is the cheapest.
 
     python tools/quad_frames.py
 """
