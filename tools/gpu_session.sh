@@ -69,25 +69,38 @@ for s in "$@"; do
       step dist2 600 python bench.py --gpus 2 --dist-backend gloo --steps 5 --warmup 1 \
         --blocks "${DIST_BLOCKS:-262144}" > gpurun_out/dist2.json 2> gpurun_out/dist2.err
       cat gpurun_out/dist2.json ;;
-    bench)
-      step bench 600 python bench.py --steps 20 --warmup 3 > gpurun_out/bench.json \
+    bench)  # the driver's command
+      step bench 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench.json \
         2> gpurun_out/bench.err
       cat gpurun_out/bench.json ;;
+    cfg2sha)
+      step cfg2sha 600 python bench.py --workload config2sha --steps 10 --warmup 2 \
+        > gpurun_out/cfg2sha.json 2> gpurun_out/cfg2sha.err
+      cat gpurun_out/cfg2sha.json ;;
+    latency)
+      step latency 300 python tools/hash_bytes_latency.py > gpurun_out/latency.log 2>&1
+      cat gpurun_out/latency.log ;;
+    sweep)  # the randomized parity cases over SWEEP_SEEDS more seeds
+      CIR_SWEEP_SEEDS=${SWEEP_SEEDS:-40} CIR_SWEEP_FIRST=${SWEEP_FIRST:-7000} step sweep 900 \
+        python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -s -k test_randomized_sweep \
+        -p no:cacheprovider --timeout 850 --timeout-method thread > gpurun_out/sweep.log 2>&1
+      tail -3 gpurun_out/sweep.log ;;
     bench_direct)
       step bench_direct 400 python bench.py --steps 10 --warmup 2 --loader direct \
         --no-cpu-baseline > gpurun_out/bench_direct.json 2> gpurun_out/bench_direct.err
       cat gpurun_out/bench_direct.json ;;
     prof)
+      # the driver's own bench command, under the profiler
       step prof 600 rocprofv3 --kernel-trace --stats --output-format csv \
-        -d gpurun_out/prof -o run -- python3 bench.py --steps 10 --warmup 2 \
-        --no-cpu-baseline > gpurun_out/prof.log 2>&1
+        -d gpurun_out/prof -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 \
+        > gpurun_out/prof.log 2>&1
       find gpurun_out/prof -name '*stats*' | head ;;
     pmc)
       for c in FETCH_SIZE WRITE_SIZE SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES \
                SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU; do
         step "pmc_$c" 600 rocprofv3 --pmc "$c" --output-format csv \
           -d "gpurun_out/pmc_$c" -o run -- python3 bench.py --steps 3 --warmup 1 \
-          --no-cpu-baseline > "gpurun_out/pmc_$c.log" 2>&1
+          --no-cpu-baseline --no-secondary > "gpurun_out/pmc_$c.log" 2>&1
       done ;;
     cfg3)
       step cfg3 600 python bench.py --workload config3 --steps 5 --warmup 1 \
