@@ -1432,12 +1432,11 @@ static hipError_t launch_desc_relay(const uint8_t* arena, const uint64_t* off,
 
 hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
                         const uint32_t* perm, uint32_t* n_long, uint64_t n, uint8_t* out,
-                        hipStream_t s, hipStream_t qs, hipStream_t aux, hipEvent_t fork,
-                        hipEvent_t qjoin, hipEvent_t ljoin, const RelayScratch* relay,
-                        const hipEvent_t* tev) {
+                        hipStream_t s, hipStream_t qs, hipEvent_t fork, hipEvent_t qjoin,
+                        const RelayScratch* relay, const hipEvent_t* tev) {
   if (n == 0) return hipSuccess;
   // tev (diagnostics): quad part start / end on its stream, lane part start /
-  // end on aux (the lane part's kernels after the gate)
+  // end on s (the lane part's kernels after the gate)
   auto mark = [&](int k, hipStream_t st) {
     return tev ? hipEventRecord(tev[k], st) : hipSuccess;
   };
@@ -1447,7 +1446,7 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
   // the most a lane-regime relay takes, in eighths of a lane wave per SIMD
   const uint32_t cap8 = (uint32_t)kRelayCap8;
   uint32_t extra = 0, groups = 0, nseg_max = 1;
-  if (relay && relay->flags && qs != s && aux != qs && desc_may_relay_slots(n, slots)) {
+  if (relay && relay->flags && qs != s && desc_may_relay_slots(n, slots)) {
     extra = (uint32_t)(n % slots);
     groups = (extra + kRelayGroupChains - 1) / kRelayGroupChains;
     if (groups > relay->groups) {
@@ -1459,7 +1458,7 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
   const uint64_t nq = std::min<uint64_t>((n + 63) / 64, quad_max_wg(n));
   const uint64_t lane_grid = grid_for(n, kThreads);
   if (lane_grid > 0x7fffffffull) return hipErrorInvalidValue;
-  const uint32_t pace = aux != qs ? kLanePace : 0u;  // only beside a concurrent quad part
+  const uint32_t pace = qs != s ? kLanePace : 0u;  // only beside a concurrent quad part
   const bool exclusive = n >= kQuadSmallBatch;
   // small batch: a relay of the chains past k whole quad waves per SIMD
   // (desc_qrelay_on decides on the device)
@@ -1467,11 +1466,11 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
   uint32_t qextra = 0;
   // (a relay runs only on the device's own quad-part stream, never on the
   // caller's: relays share the device's scratch, one stream orders them)
-  if (!exclusive && relay && relay->flags && qs != s && aux != qs &&
+  if (!exclusive && relay && relay->flags && qs != s &&
       n >= qslots &&
       n % qslots != 0 && quad_relay_fits(n % qslots, qslots))
     qextra = (uint32_t)(n % qslots);
-  // Small batches run both parts on aux, one after the other (the lane part
+  // Small batches run both parts on s, one after the other (the lane part
   // holds only chains of < 8 lines): qs only carries a relay, and without
   // one the fork to qs and the join back cost ~25 us of a 0.4 ms batch
   // (32 KiB x 16384, profiles/r02/desc/serial/)
@@ -1479,7 +1478,6 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
   const bool qs_used = qs != s && !serial;
   hipError_t e = hipEventRecord(fork, s);
   if (e == hipSuccess && qs_used) e = hipStreamWaitEvent(qs, fork, 0);
-  if (e == hipSuccess && aux != s) e = hipStreamWaitEvent(aux, fork, 0);
   if (e != hipSuccess) return e;
   if (exclusive) {
     // The quad workgroups need whole CUs (one 504-register wave per SIMD):
@@ -1493,7 +1491,7 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
     e = hipGetLastError();
     if (e == hipSuccess) e = mark(1, qs);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, aux, n_long + 1, (uint32_t)nq, 600u);
+    hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, s, n_long + 1, (uint32_t)nq, 600u);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     // unpaced batches: k_lane_rest; paced ones: k_lane_tiles (each leaves
@@ -1510,30 +1508,30 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
     // beside a relay at most two lane waves per SIMD (2 x 128 VGPRs, two
     // 64 KiB-padded workgroups per CU), so a relay wave (244) always fits;
     // the lane body is issue-bound, two waves per SIMD run it as fast
-    e = mark(2, aux);
+    e = mark(2, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads),
-                       extra ? kRelayDescLanePad : 0u, aux, arena, off, len, perm, n, n_long,
+                       extra ? kRelayDescLanePad : 0u, s, arena, off, len, perm, n, n_long,
                        (uint32_t)nq, pace, extra, (uint32_t)slots, cap8, out);
     if (pace != 0) {
       e = hipGetLastError();
       if (e != hipSuccess) return e;
-      hipLaunchKernelGGL(k_lane_tiles, dim3((unsigned)lane_grid), dim3(kThreads), 0, aux, arena,
+      hipLaunchKernelGGL(k_lane_tiles, dim3((unsigned)lane_grid), dim3(kThreads), 0, s, arena,
                          off, len, perm, n, n_long, (uint32_t)nq, pace, 0u, out);
       e = hipGetLastError();
-      if (e == hipSuccess) e = mark(3, aux);
+      if (e == hipSuccess) e = mark(3, s);
       if (e != hipSuccess) return e;
       hipLaunchKernelGGL(k_lane_tiles, dim3((unsigned)lane_grid), dim3(kThreads), 0, qs, arena,
                          off, len, perm, n, n_long, (uint32_t)nq, pace, 1u, out);
     } else {
       e = hipGetLastError();
-      if (e == hipSuccess) e = mark(3, aux);
+      if (e == hipSuccess) e = mark(3, s);
       if (e != hipSuccess) return e;
     }
   } else {
     // Every relay runs on qs (they share the device's relay scratch, so one
-    // stream orders them); the quad part runs on the lane part's stream (aux;
-    // the caller's by default) after the lane part, which is empty whenever
+    // stream orders them); the quad part runs on the lane part's stream (the
+    // caller's) after the lane part, which is empty whenever
     // the relay runs, padded to one workgroup per CU beside a relay to leave
     // room for the relay's waves.
     uint32_t qmin = 0;
@@ -1549,14 +1547,14 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
                             out, qs);
       if (e != hipSuccess) return e;
     }
-    e = mark(2, aux);
+    e = mark(2, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads), 0, aux, arena, off,
+    hipLaunchKernelGGL(k_lane_rest, dim3((unsigned)lane_grid), dim3(kThreads), 0, s, arena, off,
                        len, perm, n, n_long, (uint32_t)nq, 0u, 0u, (uint32_t)slots, 0u, out);
     e = hipGetLastError();
-    if (e == hipSuccess) e = mark(3, aux);
+    if (e == hipSuccess) e = mark(3, s);
     if (e != hipSuccess) return e;
-    hipStream_t qst = qs_used && !qextra ? qs : aux;
+    hipStream_t qst = qs_used && !qextra ? qs : s;
     e = mark(0, qst);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_quad_long<false>), dim3((unsigned)nq), dim3(kThreads),
@@ -1568,9 +1566,7 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
   }
   e = hipGetLastError();
   if (e == hipSuccess && qs_used) e = hipEventRecord(qjoin, qs);
-  if (e == hipSuccess && aux != s) e = hipEventRecord(ljoin, aux);
   if (e == hipSuccess && qs_used) e = hipStreamWaitEvent(s, qjoin, 0);
-  if (e == hipSuccess && aux != s) e = hipStreamWaitEvent(s, ljoin, 0);
   return e;
 }
 

@@ -81,16 +81,15 @@ hipError_t launch_general_desc(const uint8_t* arena, const uint64_t* off, const 
 
 // Descriptor batch in the order perm (longest chain first); the first
 // *n_long chains (device count) run in quad mode when 64 * quad_max_wg(n) hold them, on
-// qs, the rest one lane per chain on `aux`; both fork from s (`fork`) and
-// join back into s (`qjoin`, `ljoin`).
+// qs, the rest one lane per chain on s; the quad part forks from s (`fork`)
+// and joins back into it (`qjoin`).
 // relay (nullable): scratch for relaying the chains past k whole lane (or
 // quad) waves per SIMD (k_desc_relay; decided on the device).
 // tev (nullable, diagnostics): 4 timing events recorded around the quad
-// part (0, 1; on its stream) and the lane part (2, 3; on aux).
+// part (0, 1; on its stream) and the lane part (2, 3; on s).
 hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
                         const uint32_t* perm, uint32_t* n_long, uint64_t n, uint8_t* out,
-                        hipStream_t s, hipStream_t qs, hipStream_t aux, hipEvent_t fork,
-                        hipEvent_t qjoin, hipEvent_t ljoin,
+                        hipStream_t s, hipStream_t qs, hipEvent_t fork, hipEvent_t qjoin,
                         const RelayScratch* relay = nullptr,
                         const hipEvent_t* tev = nullptr);
 

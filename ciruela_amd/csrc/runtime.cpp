@@ -63,8 +63,7 @@ Device::~Device() {
   if (order_free) (void)hipEventDestroy(order_free);
   if (qstream) (void)hipStreamSynchronize(qstream);
   (void)hipFree(relay_mem);
-  if (aux_fork) (void)hipEventDestroy(aux_fork);
-  if (aux_join) (void)hipEventDestroy(aux_join);
+  if (part_fork) (void)hipEventDestroy(part_fork);
   if (q_join) (void)hipEventDestroy(q_join);
   if (qstream) (void)hipStreamDestroy(qstream);
   if (single) (void)hipStreamSynchronize(single);
@@ -182,8 +181,7 @@ static int ensure_relay(Device& d) {
 static int ensure_part_streams(Device& d) {
   if (d.order_free) return CIR_OK;
   CIR_HIP(create_part_streams(d));
-  CIR_HIP(hipEventCreateWithFlags(&d.aux_fork, hipEventDisableTiming));
-  CIR_HIP(hipEventCreateWithFlags(&d.aux_join, hipEventDisableTiming));
+  CIR_HIP(hipEventCreateWithFlags(&d.part_fork, hipEventDisableTiming));
   CIR_HIP(hipEventCreateWithFlags(&d.q_join, hipEventDisableTiming));
   CIR_HIP(hipEventCreateWithFlags(&d.order_free, hipEventDisableTiming));
   return CIR_OK;
@@ -250,7 +248,7 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
     CIR_HIP(dev::launch_sha_desc(arena, off, len, perm, n, out, s));
   else
     CIR_HIP(dev::launch_mixed(arena, off, len, perm, n_long, n, out, s, d.qstream ? d.qstream : s,
-                              s, d.aux_fork, d.q_join, d.aux_join,
+                              d.part_fork, d.q_join,
                               d.relay_mem ? &d.relay : nullptr, tev ? tev + 2 : nullptr));
   CIR_HIP(hipEventRecord(d.order_free, s));
   return CIR_OK;
@@ -716,7 +714,7 @@ int cir_hash_chunks_dev(cir_ctx* ctx, const void* d_data, uint64_t nbytes, uint6
     DeviceGuard guard;
     CIR_HIP(hipSetDevice(d->id));
     CIR_HIP(dev::launch_chunks_split((const uint8_t*)d_data, nbytes, block_size, d_out, s,
-                                     d->qstream, d->aux_fork, d->q_join, &d->relay));
+                                     d->qstream, d->part_fork, d->q_join, &d->relay));
     return CIR_OK;
   }
   CIR_HIP(dev::launch_chunks((const uint8_t*)d_data, nbytes, block_size, d_out, s));

@@ -87,7 +87,7 @@ struct Device {
   // stream: a hardware queue of its own) and its lane part on the caller's
   // stream, forked and joined with events (runtime.cpp create_part_streams).
   hipStream_t qstream = nullptr;
-  hipEvent_t aux_fork = nullptr, aux_join = nullptr, q_join = nullptr;
+  hipEvent_t part_fork = nullptr, q_join = nullptr;
   // relayed quad chains (used on qstream only; allocated at full capacity
   // by cir_init)
   dev::RelayScratch relay;
