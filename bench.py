@@ -92,14 +92,14 @@ def fill_config2(ca, data, bs, stream):
         data[16 * bs:nspecial * bs].copy_(pat.repeat((nspecial - 16) * bs // 256))
 
 
-def load_traffic(cfg_key):
-    """HBM bytes per launch from a committed PMC summary matching cfg_key."""
+def load_traffic(cfg_key, field="hbm_bytes_per_launch"):
+    """HBM bytes per launch (or per batch) from a committed PMC summary."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
         e = d.get(cfg_key)
-        return None if e is None else e.get("hbm_bytes_per_launch")
+        return None if e is None else e.get(field)
     except (OSError, ValueError):
         return None
 
@@ -362,7 +362,10 @@ def run_config3(args, ca, ctx, dev, stream):
                 "bound": "hbm", "achieved": round(algo / (total_ms / 1e3) / 1e9, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(algo / (total_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                "traffic": None, "kernel": "k_quad_long (dominant; 1 MiB chains in quad mode)",
+                "traffic": load_traffic("config3", "hbm_bytes_per_batch"),
+                "traffic_scope": "per batch: every kernel of cir_hash_blocks_dev (PMC, "
+                                 "profiles/pmc_traffic.json config3)",
+                "kernel": "k_quad_long (dominant; 1 MiB chains in quad mode)",
                 "kernel_ms_avg": round(quad_ms, 4), "batch_kernel_ms_avg": round(total_ms, 4),
                 "parts_ms_avg": {"ordering": round(order_ms, 4), "quad_part": round(quad_ms, 4),
                                  "lane_part": round(lane_ms, 4)},

@@ -14,11 +14,14 @@
 //                      --append SRC:/DEST [--append-weak SRC:/DEST]
 //                      [--replace SRC:/DEST[:OLD_IMAGE_ID]] ...
 //   ciruela-index hash [--block-size N] FILE...   (per-block BlockHash list)
+#include <dirent.h>
 #include <fcntl.h>
 #include <stdio.h>
 #include <string.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <string>
 #include <vector>
@@ -45,6 +48,36 @@ static std::string hex(const uint8_t* p, size_t n) {
 static int die(int rc, const char* what) {
   fprintf(stderr, "%s: %s: %s\n", what, cir_strerror(rc), cir_last_error());
   return rc == CIR_EIO ? 1 : 2;
+}
+
+// Bytes of the regular files under path (symlinks not followed, as the scan
+// does), counted only until they reach cap.
+static uint64_t tree_bytes(const std::string& path, uint64_t cap, uint64_t acc = 0) {
+  struct stat st;
+  if (acc >= cap || lstat(path.c_str(), &st) != 0) return acc;
+  if (S_ISREG(st.st_mode)) return acc + (uint64_t)st.st_size;
+  if (!S_ISDIR(st.st_mode)) return acc;
+  DIR* d = opendir(path.c_str());
+  if (!d) return acc;
+  while (struct dirent* e = readdir(d)) {
+    if (!strcmp(e->d_name, ".") || !strcmp(e->d_name, "..")) continue;
+    acc = tree_bytes(path + "/" + e->d_name, cap, acc);
+    if (acc >= cap) break;
+  }
+  closedir(d);
+  return acc;
+}
+
+// Staging per slot: the library default (256 MiB) for large inputs; a small
+// input gets slots just big enough to hold it, so a one-shot `sync` of a few
+// MiB does not pin 3 x 256 MiB of host memory it never fills (cir_init
+// allocates the slots up front).
+static uint64_t staging_for(const std::vector<std::string>& paths) {
+  constexpr uint64_t kMax = 256ull << 20, kMin = 1ull << 20;
+  uint64_t total = 0;
+  for (const std::string& p : paths) total = tree_bytes(p, kMax, total);
+  if (total >= kMax) return 0;
+  return std::max<uint64_t>(kMin, (total + kMin - 1) / kMin * kMin);
 }
 
 struct Job {
@@ -100,8 +133,10 @@ int main(int argc, char** argv) {
       return 2;
     }
   }
+  std::vector<std::string> inputs = files;
+  for (const Job& j : jobs) inputs.push_back(j.src);
   cir_ctx* ctx = nullptr;
-  int rc = cir_init(&ctx, 0, 0);
+  int rc = cir_init(&ctx, 0, staging_for(inputs));
   if (rc) return die(rc, "cir_init");
   if (cmd == "hash") {
     for (const std::string& f : files) {

@@ -60,7 +60,11 @@ typedef struct cir_ctx cir_ctx;
 
 /* Open the devices in device_mask (bit i = HIP device i; 0 = every visible
  * device).  staging_bytes (0 = 256 MiB) sizes each device's host->device
- * staging buffer pair for the host-memory entry points. */
+ * staging slots for the host-memory entry points.  Everything a device
+ * needs is created here -- streams, the relay scratch, three staging slots of
+ * staging_bytes (pinned host + device memory each) -- and a tiny warm-up
+ * hash loads the kernels, so no later call allocates or synchronises on the
+ * device's behalf except to grow a buffer past these sizes. */
 int cir_init(cir_ctx** ctx, uint32_t device_mask, uint64_t staging_bytes);
 void cir_destroy(cir_ctx* ctx);
 int cir_device_count(void);

@@ -121,6 +121,12 @@ for s in "$@"; do
           -d "gpurun_out/pmc3_$i" -o run -- python3 bench.py --workload config3 --steps 2 \
           --warmup 1 > "gpurun_out/pmc3_$i.log" 2>&1
       done ;;
+    pmc3t)  # HBM bytes of config 3's batches (FETCH_SIZE and WRITE_SIZE, one pass each)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        step "pmc3t_$c" 300 rocprofv3 --pmc $c --output-format csv \
+          -d "gpurun_out/pmc3t_$c" -o run -- python3 bench.py --workload config3 --steps 2 \
+          --warmup 1 > "gpurun_out/pmc3t_$c.log" 2>&1
+      done ;;
     firstread)
       step firstread 600 python tools/first_read_probe.py --gib "${TREE_GIB:-16}" \
         --read-first "${READ_FIRST:-1}" > gpurun_out/firstread.log 2>&1

@@ -66,5 +66,58 @@ def main():
     print(json.dumps(ent, indent=1))
 
 
+def config3(src, tag):
+    """`pmc3t` passes: FETCH_SIZE / WRITE_SIZE summed over every kernel of a
+    config-3 batch (ordering, quad part, lane part, relay checks), per batch
+    (= per k_chain_keys dispatch), into pmc_traffic.json["config3"]."""
+    import numpy as np  # noqa: F401  (bench's layout helper needs it)
+    sys.path.insert(0, ROOT)
+    import bench
+    offs, lens, _ = bench.config3_layout()
+    algo = int(lens.astype("int64").sum()) + 32 * int(lens.size)
+    dst = os.path.join(ROOT, "profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+    vals, per_kernel = {}, {}
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        f = os.path.join(src, "pmc3t_" + c, "run_counter_collection.csv")
+        shutil.copy(f, os.path.join(dst, "pmc3t_%s.csv" % c))
+        total, batches = 0.0, set()
+        for row in csv.DictReader(open(f)):
+            name = row["Kernel_Name"]
+            if "k_fill_splitmix64" in name or "__amd_rocclr" in name:
+                continue
+            if "k_chain_keys" in name:
+                batches.add(row["Dispatch_Id"])
+            v = float(row["Counter_Value"])
+            total += v
+            short = name.split("(")[0].split("::")[-1]
+            per_kernel.setdefault(c, {})
+            per_kernel[c][short] = per_kernel[c].get(short, 0.0) + v
+        vals[c] = total / max(1, len(batches))
+        for k in per_kernel[c]:
+            per_kernel[c][k] /= max(1, len(batches))
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    out = json.load(open(path)) if os.path.isfile(path) else {}
+    ent = {
+        "hbm_bytes_per_batch": int(vals["FETCH_SIZE"] * 1024 * 2 + vals["WRITE_SIZE"] * 1024),
+        "algorithmic_bytes_per_batch": algo,
+        "FETCH_SIZE_kb": vals["FETCH_SIZE"], "WRITE_SIZE_kb": vals["WRITE_SIZE"],
+        "per_kernel_kb": per_kernel,
+        "correction": "hbm = FETCH_SIZE*1024*2 + WRITE_SIZE*1024 (the gfx950 factor 2 is "
+                      "calibrated for wide coalesced streams, MI355X_MICROARCH.md HBM; the "
+                      "lane part reads 16 B per lane from lane-private lines, uncalibrated)",
+        "source": "profiles/%s/pmc3t_*.csv (rocprofv3 --pmc, one counter per pass, "
+                  "bench.py --workload config3 --steps 2 --warmup 1)" % tag,
+    }
+    out["config3"] = ent
+    with open(path, "w") as fh:
+        json.dump(out, fh, indent=1)
+        fh.write("\n")
+    print(json.dumps(ent, indent=1))
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 3 and sys.argv[3] == "config3":
+        config3(sys.argv[1], sys.argv[2])
+    else:
+        main()
