@@ -127,6 +127,13 @@ for s in "$@"; do
           -d "gpurun_out/pmc3t_$c" -o run -- python3 bench.py --workload config3 --steps 2 \
           --warmup 1 > "gpurun_out/pmc3t_$c.log" 2>&1
       done ;;
+    pmcreq)  # read requests by size (the terms of FETCH_SIZE), config 2 and config 3
+      step pmcreq_c2 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_BUBBLE_sum TCC_EA0_RDREQ_32B_sum \
+        TCC_EA0_RDREQ_DRAM_sum --output-format csv -d gpurun_out/pmcreq_c2 -o run -- python3 bench.py \
+        --steps 3 --warmup 1 --no-cpu-baseline --no-secondary > gpurun_out/pmcreq_c2.log 2>&1
+      step pmcreq_c3 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_BUBBLE_sum TCC_EA0_RDREQ_32B_sum \
+        TCC_EA0_RDREQ_DRAM_sum --output-format csv -d gpurun_out/pmcreq_c3 -o run -- python3 bench.py \
+        --workload config3 --steps 2 --warmup 1 > gpurun_out/pmcreq_c3.log 2>&1 ;;
     firstread)
       step firstread 600 python tools/first_read_probe.py --gib "${TREE_GIB:-16}" \
         --read-first "${READ_FIRST:-1}" > gpurun_out/firstread.log 2>&1
