@@ -66,49 +66,74 @@ def main():
     print(json.dumps(ent, indent=1))
 
 
+def batch_rows(f):
+    """Rows of a config-3 PMC csv that belong to the bench's batches: those
+    after the splitmix64 fill (cir_init's warm-up hashes come before it),
+    without the fill and the runtime's copy/fill kernels."""
+    rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Dispatch_Id"]))
+    fill = min(int(r["Dispatch_Id"]) for r in rows if "k_fill_splitmix64" in r["Kernel_Name"])
+    return [r for r in rows if int(r["Dispatch_Id"]) > fill and "__amd_rocclr" not in r["Kernel_Name"]]
+
+
 def config3(src, tag):
     """`pmc3t` passes: FETCH_SIZE / WRITE_SIZE summed over every kernel of a
     config-3 batch (ordering, quad part, lane part, relay checks), per batch
-    (= per k_chain_keys dispatch), into pmc_traffic.json["config3"]."""
-    import numpy as np  # noqa: F401  (bench's layout helper needs it)
+    (= per k_chain_keys dispatch), into pmc_traffic.json["config3"].  The
+    `pmcreq` pass (TCC_EA0_RDREQ / _32B / TCC_BUBBLE) shows the request size
+    behind FETCH_SIZE's factor 2 for this access pattern too."""
     sys.path.insert(0, ROOT)
     import bench
     offs, lens, _ = bench.config3_layout()
     algo = int(lens.astype("int64").sum()) + 32 * int(lens.size)
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
-    vals, per_kernel = {}, {}
+
+    def tally(f):
+        per, batches = {}, set()
+        for row in batch_rows(f):
+            name = row["Kernel_Name"]
+            if "k_chain_keys" in name:
+                batches.add(row["Dispatch_Id"])
+            short = name.split("(")[0].split("::")[-1]
+            key = (row["Counter_Name"], short)
+            per[key] = per.get(key, 0.0) + float(row["Counter_Value"])
+        nb = max(1, len(batches))
+        return {k: v / nb for k, v in per.items()}, nb
+
+    per_kernel, vals = {}, {}
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
         f = os.path.join(src, "pmc3t_" + c, "run_counter_collection.csv")
         shutil.copy(f, os.path.join(dst, "pmc3t_%s.csv" % c))
-        total, batches = 0.0, set()
-        for row in csv.DictReader(open(f)):
-            name = row["Kernel_Name"]
-            if "k_fill_splitmix64" in name or "__amd_rocclr" in name:
-                continue
-            if "k_chain_keys" in name:
-                batches.add(row["Dispatch_Id"])
-            v = float(row["Counter_Value"])
-            total += v
-            short = name.split("(")[0].split("::")[-1]
-            per_kernel.setdefault(c, {})
-            per_kernel[c][short] = per_kernel[c].get(short, 0.0) + v
-        vals[c] = total / max(1, len(batches))
-        for k in per_kernel[c]:
-            per_kernel[c][k] /= max(1, len(batches))
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    out = json.load(open(path)) if os.path.isfile(path) else {}
+        per, nb = tally(f)
+        per_kernel[c] = {k: round(v, 1) for (_, k), v in per.items()}
+        vals[c] = sum(per.values())
     ent = {
         "hbm_bytes_per_batch": int(vals["FETCH_SIZE"] * 1024 * 2 + vals["WRITE_SIZE"] * 1024),
         "algorithmic_bytes_per_batch": algo,
-        "FETCH_SIZE_kb": vals["FETCH_SIZE"], "WRITE_SIZE_kb": vals["WRITE_SIZE"],
+        "batches": nb,
+        "FETCH_SIZE_kb": round(vals["FETCH_SIZE"], 1), "WRITE_SIZE_kb": round(vals["WRITE_SIZE"], 1),
         "per_kernel_kb": per_kernel,
-        "correction": "hbm = FETCH_SIZE*1024*2 + WRITE_SIZE*1024 (the gfx950 factor 2 is "
-                      "calibrated for wide coalesced streams, MI355X_MICROARCH.md HBM; the "
-                      "lane part reads 16 B per lane from lane-private lines, uncalibrated)",
-        "source": "profiles/%s/pmc3t_*.csv (rocprofv3 --pmc, one counter per pass, "
-                  "bench.py --workload config3 --steps 2 --warmup 1)" % tag,
+        "correction": "hbm = FETCH_SIZE*1024*2 + WRITE_SIZE*1024 (MI355X_MICROARCH.md HBM)",
     }
+    ent["ratio_to_algorithmic"] = round(ent["hbm_bytes_per_batch"] / algo, 4)
+    req = os.path.join(src, "pmcreq_c3", "run_counter_collection.csv")
+    if os.path.isfile(req):
+        shutil.copy(req, os.path.join(dst, "pmcreq_c3.csv"))
+        per, _ = tally(req)
+        tot = {}
+        for (c, _), v in per.items():
+            tot[c] = tot.get(c, 0.0) + v
+        ent["read_requests_per_batch"] = {k: int(v) for k, v in sorted(tot.items())}
+        ent["read_bytes_at_128B_per_request"] = int(tot.get("TCC_EA0_RDREQ_sum", 0) * 128)
+        ent["request_note"] = ("TCC_BUBBLE (128-B requests) and TCC_EA0_RDREQ_32B read ~0, so "
+                               "FETCH_SIZE tallies every request at 64 B; TCC_EA0_RDREQ x 128 B "
+                               "matches the bytes read, as for config 2's k_chunks "
+                               "(pmcreq_c2.csv): the factor 2 holds for this pattern")
+    ent["source"] = ("profiles/%s/pmc3t_*.csv, pmcreq_c3.csv (rocprofv3 --pmc, one pass per "
+                     "counter set, bench.py --workload config3 --steps 2 --warmup 1; the "
+                     "dispatches of cir_init's warm-up and the data fill excluded)" % tag)
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    out = json.load(open(path)) if os.path.isfile(path) else {}
     out["config3"] = ent
     with open(path, "w") as fh:
         json.dump(out, fh, indent=1)
