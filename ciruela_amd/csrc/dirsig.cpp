@@ -2,6 +2,7 @@
 // interfaces this restates.
 #include "dirsig.hpp"
 
+#include <stdlib.h>
 #include <string.h>
 
 namespace cir {
@@ -118,13 +119,15 @@ void Emitter::add_symlink(const std::string& name, const std::string& target) {
   body_ += '\n';
 }
 
-std::string Emitter::finish(const uint8_t* footer, size_t footer_len) const {
-  std::string out;
-  out.reserve(header_.size() + body_.size() + 2 * footer_len + 1);
-  out += header_;
-  out += body_;
-  out += to_hex(footer, footer_len);
-  out += '\n';
+uint8_t* Emitter::finish_malloc(const uint8_t* footer, size_t footer_len, size_t* len) const {
+  const std::string tail = to_hex(footer, footer_len) + '\n';
+  const size_t n = header_.size() + body_.size() + tail.size();
+  uint8_t* out = (uint8_t*)malloc(n);
+  if (!out) return nullptr;
+  memcpy(out, header_.data(), header_.size());
+  memcpy(out + header_.size(), body_.data(), body_.size());
+  memcpy(out + header_.size() + body_.size(), tail.data(), tail.size());
+  *len = n;
   return out;
 }
 

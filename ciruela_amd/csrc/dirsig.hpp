@@ -39,7 +39,7 @@ struct Header {
 };
 
 // Streaming emitter: header, then for each directory start_dir + entries;
-// finish() needs the footer digest of body() (computed by the caller on
+// finish_malloc() needs the footer digest of body() (computed by the caller on
 // the GPU) and appends its hex line.
 class Emitter {
  public:
@@ -50,7 +50,8 @@ class Emitter {
   void add_symlink(const std::string& name, const std::string& target);
   // Bytes the footer hashes: everything after the header line.
   const std::string& body() const { return body_; }
-  std::string finish(const uint8_t* footer, size_t footer_len) const;
+  // header + body + hex footer + newline in one malloc'd buffer (free()); null if out of memory
+  uint8_t* finish_malloc(const uint8_t* footer, size_t footer_len, size_t* len) const;
   const std::string& header_line() const { return header_; }
 
  private:

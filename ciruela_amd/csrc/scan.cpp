@@ -513,7 +513,7 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
         em.add_file(it.name, it.exe, f.size, digests.data() + 32 * f.first_blk, nb);
       }
     }
-    return incremental ? chain.advance(em.body(), (size_t)1 << 20) : (int)CIR_OK;
+    return incremental ? chain.advance(em.body(), (size_t)256 << 10) : (int)CIR_OK;
   };
   const double t1 = trace_on() ? now_ms() : 0;
   rc = hash_files(ctx, files, block_size, threads, hash_type, digests, emit_ready);
@@ -535,17 +535,14 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
   }
   if (rc) return rc;
   const double t4 = trace_on() ? now_ms() : 0;
-  const std::string out = em.finish(footer, 32);
-  *index_out = (uint8_t*)malloc(out.size());
+  *index_out = em.finish_malloc(footer, 32, len_out);
   if (!*index_out) return fail(CIR_ENOMEM, "malloc");
-  memcpy(*index_out, out.data(), out.size());
-  *len_out = out.size();
   if (trace_on())
     fprintf(stderr,
             "cir_scan phases: walk %.1f ms, hash loop %.1f ms, last emit %.1f ms, footer %.1f ms, "
             "output %.1f ms; %zu files, index %.1f MiB\n",
             t1 - t0, t2 - t1, t3 - t2, t4 - t3, now_ms() - t4, files.size(),
-            out.size() / 1048576.0);
+            *len_out / 1048576.0);
   return CIR_OK;
 }
 
@@ -602,11 +599,8 @@ int cir_index_rewrite(cir_ctx* ctx, const uint8_t* in, size_t len, uint8_t** out
   int rc = cir_hash_blocks_ht(ctx, ht, body.empty() ? &empty : (const uint8_t*)body.data(), &off,
                               &blen, 1, footer);
   if (rc) return rc;
-  const std::string res = em.finish(footer, 32);
-  *out = (uint8_t*)malloc(res.size());
+  *out = em.finish_malloc(footer, 32, out_len);
   if (!*out) return fail(CIR_ENOMEM, "malloc");
-  memcpy(*out, res.data(), res.size());
-  *out_len = res.size();
   return CIR_OK;
 }
 

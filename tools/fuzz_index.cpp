@@ -59,7 +59,11 @@ std::string build(const Header& h, const std::vector<std::pair<std::string, std:
   }
   uint8_t footer[32];
   for (auto& b : footer) b = (uint8_t)rng();
-  return em.finish(footer, 32);
+  size_t n = 0;
+  uint8_t* p = em.finish_malloc(footer, 32, &n);
+  std::string out((const char*)p, n);
+  free(p);
+  return out;
 }
 
 int roundtrip_case() {
