@@ -145,11 +145,12 @@ for s in "$@"; do
         echo "$lib $(cat gpurun_out/cfg3ab.json)"
       done ;;
     cfg5ab)  # config 5 (one tree, kept) and config 2 from host, alternating abtest/*.so
-      for rep in 1 2; do
+      for rep in $(seq 1 "${REPS:-2}"); do
         for lib in abtest/*.so; do
           CIRUELA_AMD_LIB=$PWD/$lib step "cfg5_$lib" 600 python bench.py --workload config5 --steps 3 \
             --tree-gib "${TREE_GIB:-32}" > gpurun_out/cfg5ab.json 2> gpurun_out/cfg5ab.err
           echo "cfg5 $rep $lib $(grep -o '"value": [0-9.]*\|"seconds_all": \[[0-9., ]*\]' gpurun_out/cfg5ab.json | head -2 | tr '\n' ' ')"
+          [ -n "${CFG5_ONLY:-}" ] && continue
           CIRUELA_AMD_LIB=$PWD/$lib step "c2h_$lib" 600 python bench.py --workload config2host --steps 3 \
             --host-gib "${HOST_GIB:-16}" > gpurun_out/c2hab.json 2> gpurun_out/c2hab.err
           echo "c2h $rep $lib $(grep -o '"value": [0-9.]*\|"seconds_all": \[[0-9., ]*\]' gpurun_out/c2hab.json | head -2 | tr '\n' ' ')"
