@@ -1554,14 +1554,13 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
     e = hipGetLastError();
     if (e == hipSuccess) e = mark(3, s);
     if (e != hipSuccess) return e;
-    hipStream_t qst = qs_used && !qextra ? qs : s;
-    e = mark(0, qst);
+    e = mark(0, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_quad_long<false>), dim3((unsigned)nq), dim3(kThreads),
-                       qextra ? kRelayQuadPad : 0u, qst, arena, off, len, perm, n_long,
+                       qextra ? kRelayQuadPad : 0u, s, arena, off, len, perm, n_long,
                        (uint32_t)nq, out, n, qextra, qmin);
     e = hipGetLastError();
-    if (e == hipSuccess) e = mark(1, qst);
+    if (e == hipSuccess) e = mark(1, s);
     if (e != hipSuccess) return e;
   }
   e = hipGetLastError();

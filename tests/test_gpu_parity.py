@@ -401,6 +401,28 @@ def test_scan_vs_oracle(gpu, small_ctx, tmp_path):
     assert gpu.v1.scan(cfg, context=small_ctx) == dirsig_oracle.scan(str(tmp_path), 4096)
 
 
+@pytest.mark.parametrize("block_size,hash_name", [
+    (1, "blake2b/256"), (100, "blake2b/256"), (127, "blake2b/256"), (129, "blake2b/256"),
+    (65537, "blake2b/256"), ((1 << 20) + 7, "blake2b/256"), (129, "sha512/256"),
+    (65537, "sha512/256")])
+def test_scan_odd_block_sizes(gpu, small_ctx, tmp_path, block_size, hash_name):
+    """v1::scan with block sizes that are not multiples of the 128-B line
+    (every block then ends in a partial line; size 1 makes one chain per byte)
+    and above the staging granularity, against the scan oracle."""
+    if block_size == 1:  # one digest (65 index bytes) per file byte: a small tree
+        (tmp_path / "d").mkdir()
+        for i, n in enumerate((0, 1, 2, 127, 128, 129, 300)):
+            (tmp_path / "d" / ("f%d" % i)).write_bytes(os.urandom(n))
+        (tmp_path / "top").write_bytes(b"xyz")
+    else:
+        make_tree(tmp_path)
+    ht = gpu.HashType.blake2b_256() if hash_name == "blake2b/256" else gpu.HashType.sha512_256()
+    cfg = gpu.ScannerConfig.new().block_size(block_size).threads(4).hash(ht)
+    cfg.add_dir(str(tmp_path), "/")
+    want = dirsig_oracle.scan(str(tmp_path), block_size, hash_name)
+    assert gpu.v1.scan(cfg, context=small_ctx) == want
+
+
 def test_sync_flow_register_and_serve(gpu, small_ctx, tmp_path):
     """scan -> register_index -> register_dir -> read_block of every block
     (src/client/sync/uploads.rs:70-78), and the daemon-side invariant
