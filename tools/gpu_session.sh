@@ -218,6 +218,9 @@ for s in "$@"; do
     ubench)
       step ubench 300 ./build/valu_ubench > gpurun_out/ubench.log 2>&1
       cat gpurun_out/ubench.log ;;
+    xcdclk)  # is the shader clock per XCD? (tools/xcd_clock_probe.hip)
+      step xcdclk 120 ./build/xcd_clock_probe > gpurun_out/xcdclk.log 2>&1
+      cat gpurun_out/xcdclk.log ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
