@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace cir {
 namespace dev {
 
@@ -125,14 +127,36 @@ __device__ __forceinline__ void g4(uint64_t& a0, uint64_t& a1, uint64_t& a2, uin
   g4(v0, v1, v2, v3, v5, v6, v7, v4, v10, v11, v8, v9, v15, v12, v13, v14, m[s8], m[s10],       \
      m[s12], m[s14], m[s9], m[s11], m[s13], m[s15]);
 
+struct NoHook {
+  __device__ __forceinline__ void operator()() const {}
+};
+
+// after_col0() runs between round 0's column step (message words 0-7) and
+// its diagonal step (words 8-15): a loader can leave the second half of the
+// line's LDS reads in flight under the first G step.
+template <typename Hook = NoHook>
 __device__ __forceinline__ void compress_sm(uint64_t h[8], const uint64_t m[16], uint64_t t,
-                                            bool last) {
+                                            bool last, Hook after_col0 = Hook()) {
   uint64_t v0 = h[0], v1 = h[1], v2 = h[2], v3 = h[3];
   uint64_t v4 = h[4], v5 = h[5], v6 = h[6], v7 = h[7];
   uint64_t v8 = CIR_IV0, v9 = CIR_IV1, v10 = CIR_IV2, v11 = CIR_IV3;
   uint64_t v12 = CIR_IV4 ^ t, v13 = CIR_IV5;
   uint64_t v14 = last ? ~CIR_IV6 : CIR_IV6, v15 = CIR_IV7;
-  CIR_ROUND_SM(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
+  g4(v0, v1, v2, v3, v4, v5, v6, v7, v8, v9, v10, v11, v12, v13, v14, v15, m[0], m[2], m[4],
+     m[6], m[1], m[3], m[5], m[7]);
+  if constexpr (!std::is_same_v<Hook, NoHook>) {
+    // the column step's results are materialised here, so the compiler
+    // cannot sink it past the hook's wait and branch
+    asm volatile("" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5), "+v"(v6),
+                 "+v"(v7));
+    asm volatile("" : "+v"(v8), "+v"(v9), "+v"(v10), "+v"(v11), "+v"(v12), "+v"(v13),
+                 "+v"(v14), "+v"(v15));
+    sched_fence();
+    after_col0();
+    sched_fence();
+  }
+  g4(v0, v1, v2, v3, v5, v6, v7, v4, v10, v11, v8, v9, v15, v12, v13, v14, m[8], m[10],
+     m[12], m[14], m[9], m[11], m[13], m[15]);
   CIR_ROUND_SM(14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3)
   CIR_ROUND_SM(11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4)
   CIR_ROUND_SM(7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8)

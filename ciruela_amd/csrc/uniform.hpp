@@ -85,10 +85,15 @@ __device__ __forceinline__ void uniform_glds_wave(const uint8_t* __restrict__ ws
       m[2 * c] = mk64(x.x, x.y);
       m[2 * c + 1] = mk64(x.z, x.w);
     }
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): reads done before the refill
-    if (i + 1 < lines) issue(i + 1);
     const bool last = i + 1 == lines;
-    compress(h, m, (uint64_t)(i + 1) * 128u, last);
+    // The next line's DMA goes out after round 0's column step, which needs
+    // only chunks 0-3: chunks 4-7 land under it instead of the wave waiting
+    // for all eight reads (round 3: config 2 -1.2 to -1.4 % per launch,
+    // in-process A/B on two boxes, profiles/r03_s2/ab_overlap.log).
+    compress_sm(h, m, (uint64_t)(i + 1) * 128u, last, [&] {
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): reads done before the refill
+      if (i + 1 < lines) issue(i + 1);
+    });
   }
   if (!kPartial || lane < nv) store_digest(out + lane * 32u, h);
 }

@@ -218,6 +218,17 @@ for s in "$@"; do
     ubench)
       step ubench 300 ./build/valu_ubench > gpurun_out/ubench.log 2>&1
       cat gpurun_out/ubench.log ;;
+    lanepmc)  # 1 M x 32 KiB as a chunk-form file (k_chunks, LDS-DMA) vs descriptors (k_lane_rest)
+      for mode in 0 1; do
+        SWEEP_DESC=$mode SWEEP_ONLY=32768:1048576 SWEEP_STEPS=10 step "lane_t$mode" 300 \
+          python3 tools/shape_sweep.py > "gpurun_out/lane_t$mode.log" 2>&1
+        cat "gpurun_out/lane_t$mode.log"
+        SWEEP_DESC=$mode SWEEP_ONLY=32768:1048576 SWEEP_STEPS=3 step "lanepmc_$mode" 300 \
+          rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_WAVES SQ_INSTS_VMEM \
+          --output-format csv -d "gpurun_out/lanepmc_$mode" -o run -- python3 tools/shape_sweep.py \
+          > "gpurun_out/lanepmc_$mode.log" 2>&1
+      done
+      step counters 120 rocprofv3 -L > gpurun_out/counters.txt 2>&1 ;;
     xcdclk)  # is the shader clock per XCD? (tools/xcd_clock_probe.hip)
       step xcdclk 120 ./build/xcd_clock_probe > gpurun_out/xcdclk.log 2>&1
       cat gpurun_out/xcdclk.log ;;
