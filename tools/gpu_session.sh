@@ -218,6 +218,11 @@ for s in "$@"; do
     ubench)
       step ubench 300 ./build/valu_ubench > gpurun_out/ubench.log 2>&1
       cat gpurun_out/ubench.log ;;
+    pmcsq)  # one pass of SQ counters + GRBM over config 2 (k_chunks and the register-only k_compress_only)
+      step pmcsq 300 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY \
+        SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_ANY GRBM_GUI_ACTIVE \
+        --output-format csv -d gpurun_out/pmcsq -o run -- python3 bench.py --steps 3 --warmup 1 \
+        --no-cpu-baseline --no-secondary > gpurun_out/pmcsq.log 2>&1 ;;
     lanepmc)  # 1 M x 32 KiB as a chunk-form file (k_chunks, LDS-DMA) vs descriptors (k_lane_rest)
       for mode in 0 1; do
         SWEEP_DESC=$mode SWEEP_ONLY=32768:1048576 SWEEP_STEPS=10 step "lane_t$mode" 300 \
