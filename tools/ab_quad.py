@@ -10,6 +10,8 @@ Workloads (all device-resident, HIP events on one stream, interleaved rounds):
          cir_hash_blocks_dev (k_quad_long, small-batch policy);
   d1m    16384 x 1 MiB descriptors, same path;
   one    a single 16 MiB chain (one descriptor: the index-footer shape).
+AB_LANE=1: cfg3 plus lane-part batches -- dl32k 1 M x 32 KiB and dl4k 8 M x
+4 KiB descriptors, c3short config 3's 4 KiB / 32 KiB classes alone.
 Checks that every library produces the same digests.
 """
 import ctypes
@@ -67,7 +69,21 @@ def main():
             ctx, data.data_ptr(), o.data_ptr(), ln.data_ptr(), nblk, out.data_ptr(),
             s.cuda_stream))
     keep = []
-    if os.environ.get("AB_FIT"):  # fixed cost vs per-line cost of the small-batch quad path
+    if os.environ.get("AB_LANE"):  # lane-part workloads (descriptor batches without quad chains)
+        for name in ("1m", "4m"):
+            del work[name]
+        work["dl32k"] = desc(1 << 20, 32768)
+        work["dl4k"] = desc(8 << 20, 4096)
+        # the config-3 short classes alone, shuffled and ragged (lane part only)
+        short = lens < (1 << 20)
+        o3, l3 = torch.from_numpy(offs[short]).cuda(), torch.from_numpy(lens[short]).cuda()
+        keep.append((o3, l3))
+        ns = int(short.sum())
+        work["c3short"] = (ns, int(lens[short].astype("int64").sum()),
+                           lambda lib, ctx, out: lib.cir_hash_blocks_dev(
+                               ctx, data.data_ptr(), o3.data_ptr(), l3.data_ptr(), ns,
+                               out.data_ptr(), s.cuda_stream))
+    elif os.environ.get("AB_FIT"):  # fixed cost vs per-line cost of the small-batch quad path
         work.clear()
         for lines in (8, 32, 128, 512, 2048):
             work["d%dL" % lines] = desc(8192, 128 * lines)

@@ -32,6 +32,11 @@ for s in "$@"; do
     abquad)
       step abquad 600 python tools/ab_quad.py abtest/*.so > gpurun_out/abquad.log 2>&1
       cat gpurun_out/abquad.log ;;
+    abquadtrace)  # kernel trace of ab_quad.py over the first abtest/*.so only
+      lib=$(ls abtest/*.so | head -1)
+      step abquadtrace 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/abqt \
+        -o run -- python3 tools/ab_quad.py "$lib" > gpurun_out/abquadtrace.log 2>&1
+      cat gpurun_out/abquadtrace.log | grep -v amdgpu.ids ;;
     h2d)
       step h2d 300 python tools/h2d_probe.py > gpurun_out/h2d.log 2>&1
       HSA_ENABLE_SDMA=0 step h2d_blit 300 python tools/h2d_probe.py > gpurun_out/h2d_blit.log 2>&1
@@ -223,6 +228,14 @@ for s in "$@"; do
         SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_ANY GRBM_GUI_ACTIVE \
         --output-format csv -d gpurun_out/pmcsq -o run -- python3 bench.py --steps 3 --warmup 1 \
         --no-cpu-baseline --no-secondary > gpurun_out/pmcsq.log 2>&1 ;;
+    lanepmcab)  # dl32k as descriptors under one --pmc pass per abtest/*.so (clock + cycles)
+      for lib in abtest/*.so; do
+        n=$(basename "$lib" .so)
+        CIRUELA_AMD_LIB=$PWD/$lib SWEEP_DESC=1 SWEEP_ONLY=32768:1048576 SWEEP_STEPS=3 step "lpmc_$n" 300 \
+          rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU \
+          SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_ANY GRBM_GUI_ACTIVE --output-format csv \
+          -d "gpurun_out/lpmc_$n" -o run -- python3 tools/shape_sweep.py > "gpurun_out/lpmc_$n.log" 2>&1
+      done ;;
     lanepmc)  # 1 M x 32 KiB as a chunk-form file (k_chunks, LDS-DMA) vs descriptors (k_lane_rest)
       for mode in 0 1; do
         SWEEP_DESC=$mode SWEEP_ONLY=32768:1048576 SWEEP_STEPS=10 step "lane_t$mode" 300 \
