@@ -107,6 +107,12 @@ for s in "$@"; do
           -d "gpurun_out/pmc_$c" -o run -- python3 bench.py --steps 3 --warmup 1 \
           --no-cpu-baseline --no-secondary > "gpurun_out/pmc_$c.log" 2>&1
       done ;;
+    pmct)  # HBM bytes of config 2's k_chunks (FETCH_SIZE and WRITE_SIZE, one pass each)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        step "pmct_$c" 300 rocprofv3 --pmc $c --output-format csv -d "gpurun_out/pmct_$c" -o run \
+          -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-secondary \
+          > "gpurun_out/pmct_$c.log" 2>&1
+      done ;;
     cfg3)
       step cfg3 600 python bench.py --workload config3 --steps 5 --warmup 1 \
         > gpurun_out/cfg3.json 2> gpurun_out/cfg3.err
