@@ -39,6 +39,19 @@ def test_exports_every_declared_symbol():
     assert decl <= set(_native.EXPORTED) | {"cir_init"}
 
 
+def test_integration_binds_every_entry_point():
+    """INTEGRATION.md's Rust extern block declares every product entry point
+    of the header (test-data and cir_debug_* exports aside)."""
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    block = text[text.index('extern "C" {'):]
+    block = block[:block.index("\n}\n")]
+    bound = set(re.findall(r"pub fn (cir_[a-z0-9_]+)\(", block))
+    product = {s for s in declared_symbols()
+               if not s.startswith("cir_debug_") and s != "cir_fill_splitmix64_dev"}
+    assert product - bound == set()
+    assert bound - declared_symbols() == set()
+
+
 def test_library_is_gfx950_code():
     """The embedded fat binary carries gfx950 code objects (and only those)."""
     blob = open(_native.LIB_PATH, "rb").read()
