@@ -91,11 +91,14 @@ def main():
         work["d32k"] = desc(8192, 32768)
         work["d1m"] = desc(16384, 1 << 20)
         work["one"] = desc(1, 16 << 20)
+    if os.environ.get("AB_ONLY"):  # comma-separated workload names
+        keep_names = os.environ["AB_ONLY"].split(",")
+        work = {k: v for k, v in work.items() if k in keep_names}
     torch.cuda.synchronize()
     for name, (nblk, nb, call) in work.items():
         outs = [torch.empty(32 * nblk, dtype=torch.uint8, device="cuda:0") for _ in libs]
         times = [[] for _ in libs]
-        for rnd in range(5):
+        for rnd in range(int(os.environ.get("AB_ROUNDS", "5"))):
             for k, (lib, ctx) in enumerate(libs):
                 for rep in range(3):
                     e0 = torch.cuda.Event(enable_timing=True)
