@@ -81,3 +81,37 @@ def test_quad_dpp_instructions_are_8_byte_aligned(tmp_path, short):
         assert dpp, name
         bad = [(hex(a), ins) for a, ins in dpp if a is None or a % 8]
         assert not bad, (name, len(bad), len(dpp), bad[:3])
+
+
+def test_hot_loop_reads_overlap_round_zero(tmp_path):
+    """k_chunks' line loop issues the next line's LDS-DMA only after round
+    0's column step (blake2b_dev.hpp compress_sm hook, uniform.hpp): between
+    the last of the line's eight ds_read_b128 and the first following
+    global_load_lds there is a whole G step of VALU work (about 80
+    instructions), and no lgkmcnt(0) wait right after the reads.  The overlap
+    is worth 1.2-1.4 % of config 2 (profiles/r03_s2/ab_overlap.log)."""
+    table = codeobj.disassembly(str(tmp_path))
+    (body,) = codeobj.find(table, "k_chunks").values()
+    reads = [i for i, ins in enumerate(body) if ins.startswith("ds_read_b128")]
+    assert len(reads) >= 16  # the full-wave and the partial-wave loops
+    checked = 0
+    i = 0
+    while i < len(reads):
+        group = [reads[i]]
+        while i + 1 < len(reads) and reads[i + 1] - group[-1] < 12:
+            i += 1
+            group.append(reads[i])
+        i += 1
+        if len(group) != 8:
+            continue
+        last = group[-1]
+        nxt = next((j for j in range(last, len(body)) if body[j].startswith("global_load_lds")),
+                   None)
+        if nxt is None:
+            continue
+        between = body[last + 1:nxt]
+        valu = [ins for ins in between if ins.startswith("v_")]
+        assert len(valu) >= 60, (last, nxt, len(valu))
+        assert "s_waitcnt lgkmcnt(0)" not in body[last + 1:last + 4], body[last + 1:last + 4]
+        checked += 1
+    assert checked >= 2
