@@ -897,6 +897,7 @@ def main():
         # traffic depends on the launch shape, not on the bytes' values
         cfg_key = "bs%d/n%d/%s" % (bs, nblk, loader_name)
         traffic = load_traffic(cfg_key)
+        cycles = load_traffic(cfg_key, "cycles")
         rec = {
             "metric": METRIC,
             "value": round(job_rate(nbytes, world, args.steps, elapsed_max), 3),
@@ -924,10 +925,20 @@ def main():
                 "kernel_ms_min": round(min(kern_ms), 4),
                 "valu_ceiling_ms": valu_ms,
                 "valu_frac": round(valu_ms / (avg_kern_s * 1e3), 4) if valu_ms else None,
+                # from the committed PMC pass (profiles/pmc_traffic.json): the
+                # register-only compression's cycles / this kernel's, and the
+                # clocks both ran at -- the gap valu_frac shows is the clock
+                "cycle_frac": cycles.get("cycle_frac") if cycles else None,
+                "clock_ghz": ({"kernel": cycles["clock_ghz_k_chunks"],
+                               "register_only": cycles["clock_ghz_k_compress_only"]}
+                              if cycles else None),
                 "note": "binding roof is integer VALU (~2.0k VALU ops per 128-B "
                         "compression): valu_ceiling_ms = the same number of "
                         "compressions in registers with no memory traffic, timed "
-                        "live; valu_frac = valu_ceiling_ms / kernel_ms_avg; see DESIGN.md",
+                        "live; valu_frac = valu_ceiling_ms / kernel_ms_avg; cycle_frac "
+                        "and clock_ghz from the committed PMC pass (the kernel issues "
+                        "within 1 % of the register-only cycles; the HBM stream lowers "
+                        "the clock); see DESIGN.md 4.1",
             },
             "parity": parity,
         }
