@@ -1,4 +1,4 @@
-# Generates tools/asm_g_bodies.h (python3 tools/gen_asm_g.py > tools/asm_g_bodies.h)
+# Generates tools/asm_g_bodies.h for tools/asm_g_ubench.hip (python3 tools/gen_asm_g.py > tools/asm_g_bodies.h)
 # Generate inline-asm bodies for one half-round (4 independent G) in three orders.
 def regs():
     R = {}
