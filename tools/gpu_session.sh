@@ -188,6 +188,16 @@ for s in "$@"; do
           echo "bs=$1 nblk=$2 $lib $(grep -o '"value": [0-9.]*' gpurun_out/shape.json)"
         done
       done ;;
+    cli1)  # where a one-shot `ciruela-index sync` of config 1 spends its time
+      python3 -c "import bench; bench.make_config1_tree('/tmp/cfg1_tree')"
+      for r in 1 2 3; do
+        step "hipinit$r" 60 ./build/hip_init_probe
+      done
+      for r in 1 2 3; do
+        CIR_TRACE=1 step "cli$r" 60 python3 -c "import subprocess, sys, time; t = time.time(); \
+rc = subprocess.call(['./bin/ciruela-index', 'sync', '--append', '/tmp/cfg1_tree:/bench'], \
+stdout=subprocess.DEVNULL); print('cli wall %.3f s' % (time.time() - t), file=sys.stderr); sys.exit(rc)"
+      done ;;
     cfg1)
       step cfg1 300 python bench.py --workload config1 > gpurun_out/cfg1.json 2> gpurun_out/cfg1.err
       cat gpurun_out/cfg1.json ;;
