@@ -431,7 +431,8 @@ def run_config2host(args, ca, ctx, dev, stream):
                                        "oracle_hash_chunks (Hashes::hash_file over memory); 4 "
                                        "threads = reference default --disk-threads"
                                        % (sample / GIB, sample // bs)),
-            "note": "pageable host buffer -> pinned staging (16 copy threads) -> H2D -> "
+            "note": "pageable host buffer -> pinned staging (host copy threads: min(12, 3/4 of "
+                    "the CPU share)) -> H2D -> "
                     "k_chunks -> D2H digests, double-buffered"}
 
 
@@ -554,7 +555,9 @@ def run_config5(args, ca, ctx, ctx_init_s=None):
     nbytes = nfiles * 32 * (1 << 20)
     rd_bytes, rd_s = tree_read_pass(args.tree_dir)
     rd2_bytes, rd2_s = tree_read_pass(args.tree_dir)
-    threads = int(os.environ.get("CIR_SCAN_THREADS", "16"))
+    # reader threads: the library's own choice (auto_threads: min(12, 3/4 of
+    # the process's CPU share)) unless CIR_SCAN_THREADS asks
+    threads = int(os.environ.get("CIR_SCAN_THREADS", "0"))
     cfg = ca.ScannerConfig.new().threads(threads).add_dir(args.tree_dir, "/")
     times = []
     index = None
@@ -603,7 +606,9 @@ def run_config5(args, ca, ctx, ctx_init_s=None):
                                    "on the GPU)" % (nfiles, nbytes / GIB)},
             "files": nfiles, "bytes": nbytes, "index_bytes": len(index),
             "image_id": ca.get_hash(index).hex(), "matches_oracle": index == want,
-            "tree_gen_s": round(gen_s, 1), "reader_threads": threads, "tree": args.tree_dir,
+            "tree_gen_s": round(gen_s, 1),
+            "reader_threads": threads or "auto (min(12, 3/4 of the CPU share))",
+            "tree": args.tree_dir,
             "tree_first_read": {"seconds": round(rd_s, 3), "value": round(rd_bytes / rd_s / GIB, 2),
                                 "second_pass_value": round(rd2_bytes / rd2_s / GIB, 2),
                                 "note": "plain 16-thread CPU read of the tree before the scans "

@@ -5,6 +5,8 @@
 #include "runtime.hpp"
 
 #include <errno.h>
+#include <sched.h>
+#include <stdio.h>
 #include <string.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -81,6 +83,36 @@ bool trace_enabled() {
     return v && *v && strcmp(v, "0") != 0;
   }();
   return on;
+}
+
+// 12 vs 16 in one lease, alternating builds (profiles/r03_s2/cfg5_threads/
+// ab_copy_threads_12_vs_16.log): config 5 43.7 / 38.5 vs 38.3 / 35.3 GiB/s,
+// config 2 from host memory 51.0 / 51.7 vs 50.6 / 50.9.
+constexpr unsigned kMaxCopyThreads = 12;
+
+// CPUs this process may run on: the cgroup v2 CPU quota ("max" or
+// "quota period" in /sys/fs/cgroup/cpu.max), else the affinity mask.
+static unsigned usable_cpus() {
+  unsigned n = 0;
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) n = (unsigned)CPU_COUNT(&set);
+  if (n == 0) n = std::max(1u, std::thread::hardware_concurrency());
+  if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char quota[32] = {0};
+    unsigned long long period = 0;
+    if (fscanf(f, "%31s %llu", quota, &period) == 2 && strcmp(quota, "max") != 0 && period) {
+      const unsigned long long q = strtoull(quota, nullptr, 10);
+      const unsigned share = (unsigned)std::max<unsigned long long>(1, q / period);
+      n = std::min(n, share);
+    }
+    fclose(f);
+  }
+  return n;
+}
+
+unsigned host_copy_threads() {
+  static const unsigned n = std::max(1u, std::min(kMaxCopyThreads, usable_cpus() * 3u / 4u));
+  return n;
 }
 
 int Device::ensure_slot(Slot& s, uint64_t bytes, uint64_t nblk) {
@@ -304,15 +336,14 @@ static int check_device(int id) {
 
 // ---- host-memory batch: cir_hash_blocks --------------------------------
 
-// Run piece(off, len) over [0, n) in 8 MiB pieces on up to 16 host threads
+// Run piece(off, len) over [0, n) in 8 MiB pieces on host_copy_threads() host threads
 // (a staging batch is 256 MiB: one copying thread moves ~10 GB/s, the
 // upload takes ~55 GB/s).  Returns 0 or the first negative piece result;
 // a piece must return len on success.
 static int64_t parallel_pieces(uint64_t n, const std::function<int64_t(uint64_t, uint64_t)>& piece) {
   constexpr uint64_t kPiece = 8ull << 20;
   const uint64_t np = (n + kPiece - 1) / kPiece;
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const unsigned nt = (unsigned)std::min<uint64_t>(np, std::min(16u, hw));
+  const unsigned nt = (unsigned)std::min<uint64_t>(np, host_copy_threads());
   std::atomic<uint64_t> next{0};
   std::atomic<int64_t> err{0};
   auto work = [&] {
@@ -335,11 +366,10 @@ static int64_t parallel_pieces(uint64_t n, const std::function<int64_t(uint64_t,
   return err.load();
 }
 
-// fn(i0, i1) over [0, n) items in groups, on up to 16 host threads when the
+// fn(i0, i1) over [0, n) items in groups, on host_copy_threads() host threads when the
 // batch moves at least 16 MiB (bytes); one thread otherwise.
 static void parallel_items(size_t n, uint64_t bytes, const std::function<void(size_t, size_t)>& fn) {
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const unsigned nt = bytes < (16ull << 20) ? 1u : std::min(16u, hw);
+  const unsigned nt = bytes < (16ull << 20) ? 1u : host_copy_threads();
   if (nt <= 1 || n < 2) {
     fn(0, n);
     return;

@@ -68,6 +68,15 @@ struct Slot {
 // CIR_TRACE set to a non-empty value other than "0": per-batch timings on stderr.
 bool trace_enabled();
 
+// Host threads for the staged paths' copies and reads (scan readers when the
+// caller asks for auto threads, the host-memory batches' packing): at most
+// kMaxCopyThreads, and at most 3/4 of the CPUs this process may use (its
+// cgroup CPU quota, else its affinity mask), so the threads that submit the
+// uploads keep a CPU.  Config 5 on three boxes of a 16-CPU share
+// (profiles/r03_s2/cfg5_threads/): 12 readers 39.1-44.1 GiB/s, 16 readers
+// 32.2-42.1 (the uploads slowed to 6.4-6.7 ms per 256 MiB batch from 5.1-5.9).
+unsigned host_copy_threads();
+
 struct Device {
   int id = 0;
   hipStream_t compute = nullptr;

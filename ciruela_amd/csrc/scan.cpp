@@ -475,7 +475,7 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
   // The incremental footer chain is BLAKE2b (quad mode); a sha512/256 footer
   // is hashed once at the end (one lane).
   const bool incremental = hash_type == CIR_HASH_BLAKE2B_256;
-  if (threads == 0) threads = std::max(1u, std::thread::hardware_concurrency());
+  if (threads == 0) threads = host_copy_threads();  // auto_threads
 
   const double t0 = trace_on() ? now_ms() : 0;
   std::vector<PlanItem> plan;

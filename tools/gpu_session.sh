@@ -209,11 +209,12 @@ stdout=subprocess.DEVNULL); print('cli wall %.3f s' % (time.time() - t), file=sy
       rm -rf /dev/shm/ciruela_bench_tree
       cat gpurun_out/cfg5.json ;;
     cfg5sweep)
-      for t in 8 16 32; do
+      for t in ${THREADS:-8 16 32}; do
         CIR_SCAN_THREADS=$t CIR_TRACE=1 step "cfg5_t$t" 600 python bench.py --workload config5 --steps 2 \
           --tree-gib "${TREE_GIB:-8}" > gpurun_out/cfg5_t$t.json 2> gpurun_out/cfg5_t$t.err
-        cat gpurun_out/cfg5_t$t.json
-        tail -3 gpurun_out/cfg5_t$t.err
+        grep -o '"value": [0-9.]*\|"seconds_all": \[[0-9., ]*\]' gpurun_out/cfg5_t$t.json | head -2 | tr '\n' ' '
+        grep "cir_scan dev 0 slot" gpurun_out/cfg5_t$t.err | awk '{h+=$7; n++} END {printf "  mean h2d %.2f ms over %d slots\n", h/n, n}'
+        grep "cir_scan dev 0 batch" gpurun_out/cfg5_t$t.err | awk '{r+=$13; n++} END {printf "  mean read %.2f ms over %d batches\n", r/n, n}' 
       done
       rm -rf /dev/shm/ciruela_bench_tree ;;
     dist1)
