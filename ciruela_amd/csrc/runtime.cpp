@@ -596,7 +596,8 @@ static int export_hashes(const std::vector<uint8_t>& h, uint8_t** out, size_t* n
 //     device buffers, descriptor and digest buffers for a full batch) and
 //     the ordering scratch for one such batch;
 //   * one tiny chunk-form hash and one ordered descriptor batch on the
-//     compute stream, which load the code object and touch every buffer.
+//     compute stream, which load the code object and touch every buffer;
+//   * one 4 MiB upload on the staging and on the footer-chain stream.
 // Caller holds a DeviceGuard.
 static int init_device(Device& d, uint64_t staging) {
   CIR_HIP(hipSetDevice(d.id));
@@ -626,6 +627,16 @@ static int init_device(Device& d, uint64_t staging) {
                                    CIR_HASH_BLAKE2B_256, /*warm_only=*/true);
   if (rc) return rc;
   CIR_HIP(hipStreamSynchronize(d.compute));
+  // the process's first host->device copy on a stream takes 7-11 ms more
+  // than the next (profiles/r03_s2/cli/: a 10 MiB batch's upload 7.7-10.7 ms
+  // in a fresh CLI process, ~0.2 ms later): pay it here for the staging and
+  // footer-chain streams, with copies big enough to take the DMA engine path
+  const size_t warm = (size_t)std::min<uint64_t>(staging, 4ull << 20);
+  CIR_HIP(hipMemcpyAsync(s.d_data, s.h_data, warm, hipMemcpyHostToDevice, d.copy));
+  CIR_HIP(hipMemcpyAsync(d.slot[1].d_data, d.slot[1].h_data, warm, hipMemcpyHostToDevice,
+                         d.chain));
+  CIR_HIP(hipStreamSynchronize(d.copy));
+  CIR_HIP(hipStreamSynchronize(d.chain));
   return CIR_OK;
 }
 
