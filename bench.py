@@ -134,8 +134,17 @@ def host_info():
                     break
     except OSError:
         pass
+    quota = None
+    try:  # cgroup v2 CPU quota ("max" or "quota period")
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        pass
     return {"nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
-            "cpu_model": model, "cpu_share_per_gpu": CPU_SHARE_PER_GPU}
+            "cgroup_cpu_quota": quota, "cpu_model": model,
+            "cpu_share_per_gpu": CPU_SHARE_PER_GPU}
 
 
 def per_gpu_share():
