@@ -90,23 +90,30 @@ bool trace_enabled() {
 // config 2 from host memory 51.0 / 51.7 vs 50.6 / 50.9.
 constexpr unsigned kMaxCopyThreads = 12;
 
-// CPUs this process may run on: the cgroup v2 CPU quota ("max" or
-// "quota period" in /sys/fs/cgroup/cpu.max), else the affinity mask.
+// CPUs this process may run on: the affinity mask, capped by the cgroup CPU
+// quota (v2: "max" or "quota period" in /sys/fs/cgroup/cpu.max; v1:
+// cpu.cfs_quota_us / cpu.cfs_period_us, -1 = none).
 static unsigned usable_cpus() {
   unsigned n = 0;
   cpu_set_t set;
   if (sched_getaffinity(0, sizeof(set), &set) == 0) n = (unsigned)CPU_COUNT(&set);
   if (n == 0) n = std::max(1u, std::thread::hardware_concurrency());
+  long long quota = -1, period = 0;
   if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
-    char quota[32] = {0};
-    unsigned long long period = 0;
-    if (fscanf(f, "%31s %llu", quota, &period) == 2 && strcmp(quota, "max") != 0 && period) {
-      const unsigned long long q = strtoull(quota, nullptr, 10);
-      const unsigned share = (unsigned)std::max<unsigned long long>(1, q / period);
-      n = std::min(n, share);
-    }
+    char q[32] = {0};
+    if (fscanf(f, "%31s %lld", q, &period) == 2 && strcmp(q, "max") != 0)
+      quota = strtoll(q, nullptr, 10);
     fclose(f);
+  } else if (FILE* fq = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
+    if (fscanf(fq, "%lld", &quota) != 1) quota = -1;
+    fclose(fq);
+    if (FILE* fp = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+      if (fscanf(fp, "%lld", &period) != 1) period = 0;
+      fclose(fp);
+    }
   }
+  if (quota > 0 && period > 0)
+    n = std::min<unsigned>(n, (unsigned)std::max<long long>(1, quota / period));
   return n;
 }
 
