@@ -22,7 +22,7 @@ default --disk-threads) and at all host cores (<= 16).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--loader glds|direct]
     python bench.py --workload config3|config5|config1|config2host|config2sha
         (one secondary config on its own; the default N=1 line also carries
-        config3 and config2host as `secondary` records)
+        config3, config2host and config5 as `secondary` records)
     python bench.py --gpus N   (N > 1: launches N ranks itself through
         torch.distributed.run unless WORLD_SIZE is already set)
 """
@@ -66,7 +66,8 @@ def parse():
     p.add_argument("--tree-dir", default="/dev/shm/ciruela_bench_tree")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-secondary", action="store_true",
-                   help="N=1 default line without the secondary config3 / config2host records")
+                   help="N=1 default line without the secondary config3 / config2host / "
+                        "config5 records")
     p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                    help="process group of the N>1 path (nccl = RCCL; gloo for rehearsals "
                         "with several ranks per GPU)")
@@ -687,16 +688,40 @@ def run_config1(args, ca, ctx):
                     "`ciruela-index sync` process including HIP start-up"}
 
 
+def run_config5_leg(args, ca, ctx, dev, stream):
+    """Config 5 as a secondary record when the tree fits the tmpfs (skipped,
+    with the reason, when it does not); the tree is removed afterwards."""
+    import shutil
+    parent = os.path.dirname(args.tree_dir.rstrip("/")) or "/"
+    try:
+        st = os.statvfs(parent)
+        free = st.f_bavail * st.f_frsize / GIB
+    except OSError as e:
+        return {"skipped": "no tree filesystem: %s" % e, "matches_oracle": None}
+    need = args.tree_gib * 1.05 + 4
+    if free < need:
+        return {"skipped": "%s has %.1f GiB free, the %.0f GiB tree needs %.0f"
+                           % (parent, free, args.tree_gib, need), "matches_oracle": None}
+    try:
+        return run_config5(args, ca, ctx)
+    finally:
+        shutil.rmtree(args.tree_dir, ignore_errors=True)
+
+
 def run_secondary(args, ca, ctx, dev, stream):
     """The secondary BASELINE configs carried in the default N=1 line, so the
     driver's own run observes them: config 3 (mixed 4K/32K/1M descriptors,
-    device-resident) and config 2 from host memory (the PCIe-inclusive rate).
-    Each is a record of its own (value, roofline or seconds, cpu_baseline,
-    matches_oracle); a failure is recorded, not raised."""
+    device-resident), config 2 from host memory (the PCIe-inclusive rate) and
+    config 5 (the end-to-end scan of a 50 GiB tmpfs tree, when /dev/shm holds
+    it).  Each is a record of its own (value, roofline or seconds,
+    cpu_baseline, matches_oracle); a failure is recorded, not raised."""
     import copy
     import traceback
     out = {}
-    legs = (("config3", run_config3, dict(steps=min(args.steps, 10), warmup=min(args.warmup, 2))),
+    # config 5 first: after the other legs it ran 6 % slower than on its own
+    # (profiles/r03_s2/bench_cfg5/)
+    legs = (("config5", run_config5_leg, dict(steps=min(args.steps, 3))),
+            ("config3", run_config3, dict(steps=min(args.steps, 10), warmup=min(args.warmup, 2))),
             ("config2host", run_config2host, dict(steps=min(args.steps, 3))))
     for name, fn, over in legs:
         a = copy.copy(args)
@@ -970,7 +995,8 @@ def main():
             del data, out, ref_out
             torch.cuda.empty_cache()
             rec["secondary"] = run_secondary(args, ca, ctx, dev, stream)
-            if any(not r.get("matches_oracle", False) for r in rec["secondary"].values()):
+            # a skipped leg carries matches_oracle None; a failed one False
+            if any(r.get("matches_oracle", False) is False for r in rec["secondary"].values()):
                 parity = "FAIL: a secondary config differs from the oracle"
                 rec["parity"] = parity
         print(json.dumps(rec), flush=True)
