@@ -22,7 +22,7 @@ default --disk-threads) and at all host cores (<= 16).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--loader glds|direct]
     python bench.py --workload config3|config5|config1|config2host|config2sha
         (one secondary config on its own; the default N=1 line also carries
-        config3, config2host and config5 as `secondary` records)
+        config5, config3, config2host and config1 as `secondary` records)
     python bench.py --gpus N   (N > 1: launches N ranks itself through
         torch.distributed.run unless WORLD_SIZE is already set)
 """
@@ -711,9 +711,10 @@ def run_config5_leg(args, ca, ctx, dev, stream):
 def run_secondary(args, ca, ctx, dev, stream):
     """The secondary BASELINE configs carried in the default N=1 line, so the
     driver's own run observes them: config 3 (mixed 4K/32K/1M descriptors,
-    device-resident), config 2 from host memory (the PCIe-inclusive rate) and
+    device-resident), config 2 from host memory (the PCIe-inclusive rate),
     config 5 (the end-to-end scan of a 50 GiB tmpfs tree, when /dev/shm holds
-    it).  Each is a record of its own (value, roofline or seconds,
+    it) and config 1 (the 100-file / 10 MiB tree, in process and through one
+    `ciruela-index sync` process).  Each is a record of its own (value, roofline or seconds,
     cpu_baseline, matches_oracle); a failure is recorded, not raised."""
     import copy
     import traceback
@@ -722,7 +723,9 @@ def run_secondary(args, ca, ctx, dev, stream):
     # (profiles/r03_s2/bench_cfg5/)
     legs = (("config5", run_config5_leg, dict(steps=min(args.steps, 3))),
             ("config3", run_config3, dict(steps=min(args.steps, 10), warmup=min(args.warmup, 2))),
-            ("config2host", run_config2host, dict(steps=min(args.steps, 3))))
+            ("config2host", run_config2host, dict(steps=min(args.steps, 3))),
+            ("config1", lambda a, ca_, ctx_, dev_, st_: run_config1(a, ca_, ctx_),
+             dict(steps=min(args.steps, 10))))
     for name, fn, over in legs:
         a = copy.copy(args)
         for k, v in over.items():
