@@ -390,12 +390,12 @@ def make_tree(root):
 
 def test_scan_vs_oracle(gpu, small_ctx, tmp_path):
     make_tree(tmp_path)
-    for threads in (1, 4):
+    want = dirsig_oracle.scan(str(tmp_path), 32768)
+    for threads in (1, 4, 0):  # 0: auto_threads (the library's host_copy_threads)
         cfg = gpu.ScannerConfig.new().threads(threads).hash(gpu.HashType.blake2b_256())
         cfg.add_dir(str(tmp_path), "/")
         got = gpu.v1.scan(cfg, context=small_ctx)
-        want = dirsig_oracle.scan(str(tmp_path), 32768)
-        assert got == want
+        assert got == want, threads
     # block size other than the default
     cfg = gpu.ScannerConfig.new().block_size(4096).add_dir(str(tmp_path), "/")
     assert gpu.v1.scan(cfg, context=small_ctx) == dirsig_oracle.scan(str(tmp_path), 4096)
