@@ -3,7 +3,7 @@
 // Reference: `ciruela sync` (src/client/main.rs:94-99 -> src/client/sync/
 // mod.rs:168-220 -> uploads::prepare, src/client/sync/uploads.rs:61-105).
 // For every --append / --append-weak / --replace SRC:DEST it runs the scan
-// (uploads.rs:49-59, threads = --disk-threads, default 4), registers the
+// (uploads.rs:49-59, threads = --disk-threads), registers the
 // index (InMemoryIndexes::register_index -> ImageId) and prints
 //   <image id> <kind> <dest> <src>
 // Signing and the upload itself (networking, src/client/sync/network.rs) are
@@ -101,7 +101,12 @@ int main(int argc, char** argv) {
     return 2;
   }
   const std::string cmd = argv[1];
-  uint32_t threads = 4;  // GlobalOptions.threads (src/client/global_options.rs:13)
+  // --disk-threads N is GlobalOptions.threads (src/client/global_options.rs:13,
+  // default 4), the reference's CPU hashing pool.  Here the host threads
+  // only read files into the staging buffers, and 4 readers hold a large
+  // tree to ~22 GiB/s, so without the flag the library picks
+  // its reader count (0: min(12, 3/4 of the CPU share)); given, N is used.
+  uint32_t threads = 0;
   uint64_t bs = CIR_DEFAULT_BLOCK_SIZE;
   std::string index_dir;
   std::vector<Job> jobs;
