@@ -165,23 +165,25 @@ def host_fill_blocks(oracle, buf, word0, seed, block_words, first_block):
         list(ex.map(part, range(THREADS)))
 
 
-def test_config4_last_shard_full(gpu, oracle):
+@pytest.mark.parametrize("rank", range(8))
+def test_config4_shard_full(gpu, oracle, rank):
     """Config 4 (BASELINE.json configs[3]): 256 GiB of 32 KiB
     blocks range-split over 8 GPUs, rank g owning global blocks
     [g*2^20, (g+1)*2^20), block i filled with splitmix64 seeded
     0x5EED0004 ^ i -- exactly as bench.py's N>1 path fills HBM
-    (bench.shard + cir_fill_splitmix64_dev).  The last rank's full 32 GiB
-    shard (first block 7 * 2^20) is hashed through cir_hash_chunks_dev and
-    EVERY digest is checked against the threaded oracle, which regenerates
-    each block from its global index alone."""
+    (bench.shard + cir_fill_splitmix64_dev).  Each rank's full 32 GiB shard
+    is hashed here, one after another on the one GPU, through
+    cir_hash_chunks_dev, and EVERY digest is checked against the threaded
+    oracle, which regenerates each block from its global index alone: the
+    eight cases together check all 8,388,608 digests of config 4."""
     import sys
     import torch
     from conftest import ROOT
     sys.path.insert(0, ROOT)
     import bench
-    nblk, world, rank = 1 << 20, 8, 7
+    nblk, world = 1 << 20, 8
     first, count = bench.shard(rank, world, nblk)
-    assert (first, count) == (7 << 20, 1 << 20)
+    assert (first, count) == (rank << 20, 1 << 20)
     nbytes = count * BS
     data = torch.empty(nbytes, dtype=torch.uint8, device="cuda:0")
     gpu._n.check(gpu._n.lib.cir_fill_splitmix64_dev(data.data_ptr(), nbytes, SEED_C4, BS, first,
