@@ -17,7 +17,8 @@ committed rocprofv3 PMC summary (profiles/) when one matches this config.
 cpu_baseline: the oracle (C restatement of RFC 7693 BLAKE2b-256 +
 dir-signature's block split, "port") on the host cores of this box, over a
 bounded sample of the same config-2 blocks, at 4 threads (the reference's
-default --disk-threads) and at all host cores (<= 16).
+default --disk-threads), at the per-GPU CPU share (16) and at one thread per
+CPU of the affinity mask; the host record names the cgroup CPU quota.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--loader glds|direct]
     python bench.py --workload config3|config5|config1|config2host|config2sha
