@@ -1340,3 +1340,31 @@ def test_desc_relay_unordered_lengths_in_one_bin(gpu, ctx, oracle, regime):
         torch.cuda.synchronize()
         got = out.cpu().numpy()
         assert first_bad(got, want) is None, "descriptor %s" % first_bad(got, want)
+
+
+def test_context_lifecycle_releases_device_memory(gpu, oracle):
+    """cir_init allocates a device state's whole working set up front (three
+    staging slots, ordering and relay scratch, footer-chain buffers) and
+    cir_destroy must give all of it back.  The first two cycles of a process
+    leave ~0.2 GiB with the HIP runtime for good (its own lazily created
+    state; tools/lifecycle_probe.py: 184 + 24 MiB, then 0 per cycle), so
+    after two warm-up cycles ten more create / use / destroy cycles of a
+    64 MiB-staging context must leave the device's free memory unchanged."""
+    import torch
+    data = np.frombuffer(os.urandom(1 << 20), dtype=np.uint8)
+    want = np.empty(32 * 32, dtype=np.uint8)
+    oracle.oracle_hash_chunks(data.ctypes.data, data.size, 32768, want.ctypes.data, 4)
+
+    def cycle():
+        c = gpu.Context(device_mask=1, staging_bytes=64 << 20)
+        size, hashes = gpu.Hashes.hash_file(gpu.HashType.blake2b_256(), 32768,
+                                            data.tobytes(), context=c)
+        assert size == data.size and hashes.raw() == want.tobytes()
+        c.close()
+        torch.cuda.synchronize()
+        return torch.cuda.mem_get_info()[0]
+    cycle()
+    free0 = cycle()
+    for _ in range(10):
+        free1 = cycle()
+    assert free0 - free1 < (16 << 20), (free0 - free1) >> 20
