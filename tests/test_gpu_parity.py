@@ -1363,8 +1363,14 @@ def test_context_lifecycle_releases_device_memory(gpu, oracle):
         c.close()
         torch.cuda.synchronize()
         return torch.cuda.mem_get_info()[0]
+    def rss():
+        with open("/proc/self/status") as f:
+            return next(int(ln.split()[1]) << 10 for ln in f if ln.startswith("VmRSS:"))
     cycle()
     free0 = cycle()
+    rss0 = rss()
     for _ in range(10):
         free1 = cycle()
     assert free0 - free1 < (16 << 20), (free0 - free1) >> 20
+    # the pinned staging (3 x 64 MiB per context) goes back to the host too
+    assert rss() - rss0 < (64 << 20), (rss() - rss0) >> 20
