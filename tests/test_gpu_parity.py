@@ -96,6 +96,23 @@ def test_hash_bytes(gpu, oracle):
         assert bytes(gpu.BlockHash.hash_bytes(data)) == oracle_digest(oracle, data)
 
 
+def test_hash_bytes_from_many_threads(gpu, oracle):
+    """BlockHash::hash_bytes is called per received block by the daemon's
+    fetch futures (src/daemon/tracking/fetch_blocks.rs:77): eight host
+    threads hashing at once through the one default context (one single-shot
+    stream, serialised by its mutex; ctypes drops the GIL) all get their own
+    block's digest, sizes 0 .. 40 KiB across the single-shot buffer's
+    growth."""
+    from concurrent.futures import ThreadPoolExecutor
+    rng = random.Random(77)
+    blocks = [os.urandom(rng.choice([0, 1, 127, 128, 129, 4096, 32768, 40000]))
+              for _ in range(160)]
+    with ThreadPoolExecutor(8) as ex:
+        got = list(ex.map(lambda b: bytes(gpu.BlockHash.hash_bytes(b)), blocks))
+    for b, g in zip(blocks, got):
+        assert g == oracle_digest(oracle, b), len(b)
+
+
 @pytest.mark.parametrize("bs,nbytes", [
     # < kQuadSmallBatch blocks of >= 8 lines: quad mode (k_quad_chunks)
     (32768, 256 * 32768),
