@@ -878,6 +878,31 @@ def test_error_paths_are_codes_not_aborts(gpu, small_ctx, tmp_path):
     assert out.cpu().numpy().tobytes() == want
 
 
+@pytest.mark.skipif(os.geteuid() == 0, reason="root reads files whatever their mode")
+@pytest.mark.parametrize("what", ["file", "dir"])
+def test_scan_unreadable_entry_is_an_io_error(gpu, small_ctx, tmp_path, what):
+    """v1::scan returns io::Error for a file or directory it cannot read
+    (src/client/sync/uploads.rs:57 wraps it as "error indexing dir"): the
+    GPU scan gives CIR_EIO, after its reader threads and staging pipeline
+    have started, and the context indexes the same tree once it is readable."""
+    n = gpu._n
+    (tmp_path / "a").mkdir()
+    (tmp_path / "a" / "ok.bin").write_bytes(os.urandom(100000))
+    (tmp_path / "b").mkdir()
+    victim = tmp_path / "b" / "secret.bin"
+    victim.write_bytes(os.urandom(70000))
+    target = victim if what == "file" else tmp_path / "b"
+    os.chmod(target, 0)
+    try:
+        cfg = gpu.ScannerConfig.new().add_dir(str(tmp_path), "/")
+        with pytest.raises(n.CiruelaError) as e:
+            gpu.v1.scan(cfg, context=small_ctx)
+        assert e.value.status == n.CIR_EIO
+    finally:
+        os.chmod(target, 0o755 if what == "dir" else 0o644)
+    assert gpu.v1.scan(cfg, context=small_ctx) == dirsig_oracle.scan(str(tmp_path), 32768)
+
+
 def oracle_digest_any(b):
     import hashlib
     return hashlib.blake2b(b, digest_size=32).digest()
