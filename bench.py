@@ -966,6 +966,8 @@ def main():
                 "traffic": traffic,
                 "kernel_ms_avg": round(avg_kern_s * 1e3, 4),
                 "kernel_ms_min": round(min(kern_ms), 4),
+                # SURVEY.md 8d quotes the median of >= 10 HIP-event timed runs
+                "kernel_ms_median": round(sorted(kern_ms)[len(kern_ms) // 2], 4),
                 "valu_ceiling_ms": valu_ms,
                 "valu_frac": round(valu_ms / (avg_kern_s * 1e3), 4) if valu_ms else None,
                 # from the committed PMC pass (profiles/pmc_traffic.json): the
