@@ -115,3 +115,37 @@ def test_hot_loop_reads_overlap_round_zero(tmp_path):
         assert "s_waitcnt lgkmcnt(0)" not in body[last + 1:last + 4], body[last + 1:last + 4]
         checked += 1
     assert checked >= 2
+
+
+def test_hot_loop_instruction_budget(tmp_path):
+    """k_chunks' line loop is one compression per iteration at the G-step
+    floor: 96 G steps x (6 v_lshl_add_u64 + 8
+    v_xor_b32 + 6 v_alignbit_b32) = 1920 VALU, rot32 free, plus under 50 of
+    glue (the feed-forward as 16 v_bitop3_b32 three-way xors, the LDS read
+    addresses) -- 1958 today; the PMC count per compression
+    adds the per-chain set-up and exit work.  A compiler or source change that adds moves, spills or
+    64-bit add pairs to the loop fails here."""
+    table = codeobj.disassembly(str(tmp_path), with_addr=True)
+    (body,) = codeobj.find(table, "k_chunks").values()
+    at = {a: i for i, (a, _) in enumerate(body)}
+    loops = []
+    for i, (a, ins) in enumerate(body):
+        op = ins.split()
+        if not op[0].startswith("s_cbranch"):
+            continue
+        off = int(op[-1])
+        off = off - 65536 if off > 32767 else off
+        j = at.get(a + 4 + 4 * off)
+        if j is not None and j < i:
+            ops = [x.split()[0] for _, x in body[j:i + 1]]
+            if ops.count("ds_read_b128") == 8:
+                loops.append(ops)
+    assert len(loops) >= 2, len(loops)  # the full-wave and the partial-wave loops
+    for ops in loops:
+        valu = [o for o in ops if o.startswith("v_")]
+        assert ops.count("v_alignbit_b32") == 576
+        assert 576 <= ops.count("v_lshl_add_u64") <= 584
+        assert 768 <= ops.count("v_xor_b32_e32") + ops.count("v_xor_b32_e64") <= 776
+        assert 1920 <= len(valu) <= 1970, len(valu)
+        assert not any(o.startswith(("scratch_", "buffer_store", "v_readlane", "v_writelane"))
+                       for o in ops)
