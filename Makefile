@@ -16,7 +16,8 @@ LIB := ciruela_amd/libciruela_amd.so
 CLI := bin/ciruela-index
 
 SRCS_HIP := $(CSRC)/kernels.hip $(CSRC)/order.hip
-SRCS_CPP := $(CSRC)/runtime.cpp $(CSRC)/dirsig.cpp $(CSRC)/scan.cpp $(CSRC)/registry.cpp
+SRCS_CPP := $(CSRC)/runtime.cpp $(CSRC)/dirsig.cpp $(CSRC)/scan.cpp $(CSRC)/registry.cpp \
+            $(CSRC)/blake2b_host.cpp
 OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS_HIP)) \
         $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(SRCS_CPP))
 HDRS := $(wildcard $(CSRC)/*.hpp) include/ciruela_blockhash.h

@@ -20,12 +20,18 @@ bounded sample of the same config-2 blocks, at 4 threads (the reference's
 default --disk-threads), at the per-GPU CPU share (16) and at one thread per
 CPU of the affinity mask; the host record names the cgroup CPU quota.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--loader glds|direct]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--loader api|glds|direct]
     python bench.py --workload config3|config5|config1|config2host|config2sha
         (one secondary config on its own; the default N=1 line also carries
         config5, config3, config2host and config1 as `secondary` records)
     python bench.py --gpus N   (N > 1: launches N ranks itself through
         torch.distributed.run unless WORLD_SIZE is already set)
+    python bench.py --gpus 1 --force-dist   (the N>1 code path -- process
+        group, config 4, job-wide parity -- on one rank, launched the same way)
+
+config.entry_point names the C-ABI call the timed steps made:
+cir_hash_chunks_dev (the production path, --loader api, the default) or
+cir_debug_hash_uniform_dev (a single-kernel A/B variant, --loader glds|direct).
 """
 import argparse
 import ctypes
@@ -56,7 +62,8 @@ def parse():
     p.add_argument("--blocks", type=int, default=1 << 20, help="blocks per GPU")
     p.add_argument("--block-size", type=int, default=32768)
     p.add_argument("--loader", choices=["glds", "direct", "api"], default="api",
-                   help="api = cir_hash_chunks_dev (production path, LDS-DMA loader)")
+                   help="api = cir_hash_chunks_dev (the production path); glds / direct = "
+                        "cir_debug_hash_uniform_dev with the LDS-DMA / per-lane loader")
     p.add_argument("--workload", choices=["auto", "config3", "config5", "config1", "config2host",
                                           "config2sha"],
                    default="auto", help="auto = config2 at N=1, config4 at N>1")
@@ -77,6 +84,12 @@ def parse():
                         "prints the line skeleton with the ranks the job saw (CPU tests)")
     p.add_argument("--force-dist", action="store_true",
                    help="run the N>1 code path (process group, config 4) even at world size 1")
+    p.add_argument("--footer", choices=["host", "gpu", "ab"], default="host",
+                   help="config 5: where the index footer is hashed (cir_set_footer_mode); "
+                        "ab alternates host and gpu scans and reports both")
+    p.add_argument("--dry-run-bad-rank", type=int, default=-1,
+                   help="--dry-run only: this rank corrupts one digest of its shard (the "
+                        "job-wide parity reduction must report FAIL)")
     p.add_argument("--cpu-seconds", type=float, default=2.5,
                    help="wall seconds of the 4-thread CPU-baseline measurement (all cores: "
                         "the same CPU work)")
@@ -243,6 +256,52 @@ def max_over_ranks(seconds, device=None):
 def job_rate(bytes_per_rank_step, world, steps, elapsed_max):
     """Whole-job GiB/s: all ranks' bytes over the slowest rank's time."""
     return bytes_per_rank_step * world * steps / elapsed_max / GIB
+
+
+def entry_point(loader):
+    """(C-ABI entry point the timed steps call, kernel loader it runs) for a
+    --loader choice: the production call for "api", the A/B kernel for the
+    others.  `traffic_key` picks the committed PMC summary of that launch."""
+    if loader == "api":
+        return {"entry_point": "cir_hash_chunks_dev", "loader": "lds-dma"}
+    return {"entry_point": "cir_debug_hash_uniform_dev",
+            "loader": "lds-dma" if loader == "glds" else "direct"}
+
+
+def traffic_key(bs, nblk, loader):
+    return "bs%d/n%d/%s" % (bs, nblk, entry_point(loader)["entry_point"]
+                           if loader == "api" else "uniform-" + loader)
+
+
+def job_summary(rank_stats, device=None):
+    """Every rank's [mismatches, checked blocks, failed checks, kernel ms
+    avg, kernel ms min] gathered on every rank (one all_gather over the
+    process group; the identity at world size 1 or without one).  Returns
+    the list of per-rank rows, rank order."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(x) for x in rank_stats], dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        parts = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+        dist.all_gather(parts, t)
+    else:
+        parts = [t]
+    return [[float(v) for v in p.cpu().tolist()] for p in parts]
+
+
+def job_parity(rows, reasons=None):
+    """The line's parity over every rank's row of job_summary: "ok" only
+    when no rank found a mismatch or failed a check."""
+    bad = int(sum(r[0] for r in rows))
+    checked = int(sum(r[1] for r in rows))
+    failed = [i for i, r in enumerate(rows) if r[0] or r[2]]
+    if not failed:
+        return "ok", checked
+    msg = "FAIL: rank(s) %s: %d of %d checked digests differ" % (
+        ",".join(map(str, failed)), bad, checked)
+    if reasons:
+        msg += " (%s)" % reasons
+    return msg, checked
 
 
 def config4_check(oracle_lib, digests, nbytes, bs, first_block, sample=64):
@@ -551,6 +610,64 @@ def tree_read_pass(root, threads=16, piece=4 << 20):
     return total, time.perf_counter() - t0
 
 
+def _pct(xs, q):
+    xs = sorted(xs)
+    return xs[min(len(xs) - 1, int(round(q * (len(xs) - 1))))] if xs else None
+
+
+def _merge(ivs):
+    out = []
+    for a, b in sorted(ivs):
+        if out and a <= out[-1][1]:
+            out[-1][1] = max(out[-1][1], b)
+        else:
+            out.append([a, b])
+    return out
+
+
+def scan_batch_summary(batches, phases):
+    """Config 5's per-batch phases (cir_debug_scan_batches rows of one scan)
+    reduced to what bounds the scan: H2D time per batch -- split by whether
+    the readers were filling a slot meanwhile -- read time, the host's wait
+    for a free slot, hash + digest return, and how busy the copy engine and
+    the readers were over the hash loop."""
+    if not batches:
+        return None
+    r3 = lambda x: None if x is None else round(x, 3)  # noqa: E731
+
+    def stats(xs):
+        return {"median": r3(_pct(xs, 0.5)), "p90": r3(_pct(xs, 0.9)), "sum": r3(sum(xs))}
+    h2d = [b["h2d_end_ms"] - b["h2d_start_ms"] for b in batches]
+    read = [b["read_end_ms"] - b["read_start_ms"] for b in batches]
+    reads = _merge([(b["read_start_ms"], b["read_end_ms"]) for b in batches])
+    frac = []
+    for b, h in zip(batches, h2d):
+        ov = sum(max(0.0, min(b["h2d_end_ms"], e) - max(b["h2d_start_ms"], a)) for a, e in reads)
+        frac.append(ov / h if h > 0 else 0.0)
+    alone = [h for h, f in zip(h2d, frac) if f < 0.1]
+    busy = [h for h, f in zip(h2d, frac) if f > 0.9]
+    loop = phases.get("hash_loop_ms") or 0.0
+    mib = [b["bytes"] / (1 << 20) for b in batches]
+    return {
+        "batches": len(batches), "batch_mib_median": r3(_pct(mib, 0.5)),
+        "h2d_ms": stats(h2d),
+        "h2d_gbs_median": r3(_pct([b["bytes"] / h / 1e6 for b, h in zip(batches, h2d) if h > 0],
+                                  0.5)),
+        "h2d_ms_while_reading": {"median": r3(_pct(busy, 0.5)), "batches": len(busy)},
+        "h2d_ms_without_reads": {"median": r3(_pct(alone, 0.5)), "batches": len(alone)},
+        "h2d_read_overlap_frac_median": r3(_pct(frac, 0.5)),
+        "read_ms": stats(read),
+        "read_gbs_median": r3(_pct([b["bytes"] / r / 1e6 for b, r in zip(batches, read) if r > 0],
+                                   0.5)),
+        "wait_ms": stats([b["wait_ms"] for b in batches]),
+        "hash_d2h_ms_median": r3(_pct([b["done_ms"] - b["hash_start_ms"] for b in batches], 0.5)),
+        "copy_busy_frac": r3(sum(h2d) / loop) if loop else None,
+        "read_busy_frac": r3(sum(e - a for a, e in reads) / loop) if loop else None,
+        "first_read_ms": r3(min(b["read_start_ms"] for b in batches)),
+        "last_done_ms": r3(max(b["done_ms"] for b in batches)),
+    }
+
+
 def run_config5(args, ca, ctx, ctx_init_s=None):
     """value = best of the scans; value_first = the first scan of this
     process, which is what one `ciruela sync` sees (it scans once per run,
@@ -570,16 +687,37 @@ def run_config5(args, ca, ctx, ctx_init_s=None):
     # the process's CPU share)) unless CIR_SCAN_THREADS asks
     threads = int(os.environ.get("CIR_SCAN_THREADS", "0"))
     cfg = ca.ScannerConfig.new().threads(threads).add_dir(args.tree_dir, "/")
-    times = []
+    # footer placement: the library default (host), the GPU chain, or both
+    # alternating in one process (--footer ab); every scan is timed per batch
+    modes = {"host": ["host"], "gpu": ["gpu"], "ab": ["host", "gpu"]}[args.footer]
+    scans = []
     index = None
-    for i in range(max(1, args.steps)):
+    for i in range(max(1, args.steps) * len(modes)):
+        mode = modes[i % len(modes)]
+        ctx.set_footer_mode(ctx.FOOTER_HOST if mode == "host" else ctx.FOOTER_GPU)
+        ctx.scan_timing(True)
         t0 = time.perf_counter()
         got = ca.v1.scan(cfg, context=ctx)
-        times.append(time.perf_counter() - t0)
+        dt = time.perf_counter() - t0
+        ph = ctx.scan_phases()
+        summ = scan_batch_summary(ctx.scan_batches(), ph)
+        ctx.scan_timing(False)
+        scans.append({"footer": mode, "seconds": round(dt, 4),
+                      "phases_ms": {k: round(ph[k], 3) for k in
+                                    ("walk_ms", "hash_loop_ms", "last_emit_ms", "footer_tail_ms",
+                                     "output_ms", "footer_busy_ms")},
+                      "footer_feeds": int(ph["footer_feeds"]), "batches": summ})
         if index is not None and got != index:
             raise SystemExit("config5: two scans of the same tree differ")
         index = got
+    ctx.set_footer_mode(ctx.FOOTER_HOST)
+    times = [sc["seconds"] for sc in scans if sc["footer"] == modes[0]]
     best = min(times)
+    best_scan = min((sc for sc in scans if sc["footer"] == modes[0]), key=lambda sc: sc["seconds"])
+    by_mode = {m: {"seconds_best": min(sc["seconds"] for sc in scans if sc["footer"] == m),
+                   "value_best": round(nbytes / min(sc["seconds"] for sc in scans
+                                                   if sc["footer"] == m) / GIB, 3)}
+               for m in modes}
     # checker: the whole tree indexed again by the CPU restatement (every
     # block digest, the emitter, the footer) on all cores of the GPU's share;
     # its time is the all-cores leg of the CPU baseline on the full workload
@@ -613,8 +751,17 @@ def run_config5(args, ca, ctx, ctx_init_s=None):
             "value_first": round(nbytes / times[0] / GIB, 3),
             "context_init_s": round(ctx_init_s, 3) if ctx_init_s is not None else None,
             "config": {"workload": "config5: %d files x 32 MiB in 40 dirs (%.0f GiB) on tmpfs, "
-                                   "cir_scan_v1 (reads -> pinned -> H2D -> hash -> D2H, footer "
-                                   "on the GPU)" % (nfiles, nbytes / GIB)},
+                                   "cir_scan_v1 (reads -> pinned -> H2D -> hash -> D2H; footer "
+                                   "on %s)" % (nfiles, nbytes / GIB,
+                                               "a host thread" if modes[0] == "host"
+                                               else "the GPU chain")},
+            "footer": modes[0], "by_footer_mode": by_mode,
+            # the best scan's phases: the footer's busy time (host thread, or
+            # the summed k_chain_step time for the GPU chain) and its tail
+            # after the last batch, and the per-batch H2D / read / wait split
+            "footer_chain_ms": best_scan["phases_ms"]["footer_busy_ms"],
+            "footer_tail_ms": best_scan["phases_ms"]["footer_tail_ms"],
+            "phases_best": best_scan, "scans": scans,
             "files": nfiles, "bytes": nbytes, "index_bytes": len(index),
             "image_id": ca.get_hash(index).hex(), "matches_oracle": index == want,
             "tree_gen_s": round(gen_s, 1),
@@ -689,9 +836,28 @@ def run_config1(args, ca, ctx):
                     "`ciruela-index sync` process including HIP start-up"}
 
 
+def mem_available_gib():
+    """MemAvailable of /proc/meminfo in GiB (None if unreadable): a tmpfs
+    tree lives in RAM, whatever statvfs says about the filesystem's size."""
+    try:
+        with open("/proc/meminfo") as f:
+            for ln in f:
+                if ln.startswith("MemAvailable:"):
+                    return int(ln.split()[1]) / (1 << 20)
+    except (OSError, ValueError, IndexError):
+        pass
+    return None
+
+
+def tree_complete(root, gib, file_mib=32):
+    return os.path.exists(os.path.join(root, ".complete-%d-%d" % (int(gib * 1024 // file_mib),
+                                                                  file_mib)))
+
+
 def run_config5_leg(args, ca, ctx, dev, stream):
-    """Config 5 as a secondary record when the tree fits the tmpfs (skipped,
-    with the reason, when it does not); the tree is removed afterwards."""
+    """Config 5 as a secondary record when the tree fits the tmpfs and the
+    RAM behind it (skipped, with the reason, when it does not; a complete
+    tree left by an earlier run is reused); the tree is removed afterwards."""
     import shutil
     parent = os.path.dirname(args.tree_dir.rstrip("/")) or "/"
     try:
@@ -700,9 +866,14 @@ def run_config5_leg(args, ca, ctx, dev, stream):
     except OSError as e:
         return {"skipped": "no tree filesystem: %s" % e, "matches_oracle": None}
     need = args.tree_gib * 1.05 + 4
-    if free < need:
-        return {"skipped": "%s has %.1f GiB free, the %.0f GiB tree needs %.0f"
-                           % (parent, free, args.tree_gib, need), "matches_oracle": None}
+    if not tree_complete(args.tree_dir, args.tree_gib):
+        avail = mem_available_gib()
+        if free < need:
+            return {"skipped": "%s has %.1f GiB free, the %.0f GiB tree needs %.0f"
+                               % (parent, free, args.tree_gib, need), "matches_oracle": None}
+        if avail is not None and avail < need + 8:
+            return {"skipped": "MemAvailable %.1f GiB, the %.0f GiB tmpfs tree needs %.0f + 8"
+                               % (avail, args.tree_gib, need), "matches_oracle": None}
     try:
         return run_config5(args, ca, ctx)
     finally:
@@ -769,7 +940,13 @@ def launch_ranks(nproc, argv):
 
 def dry_run(args, rank, world):
     """The N>1 line's plumbing without a GPU: process group (gloo), shard
-    plan, timed region and max-over-ranks, one JSON line from rank 0."""
+    plan, timed region, max-over-ranks and the job-wide parity reduction,
+    one JSON line from rank 0.  Each rank's shard digests come from the
+    oracle here (there is no device; this checks the bookkeeping around the
+    hash, not the hash), then go through the same config4_check and
+    job_summary as the GPU path; --dry-run-bad-rank R corrupts one of rank
+    R's digests first."""
+    import numpy as np
     import torch
     import torch.distributed as dist
     distributed = world > 1 or args.force_dist
@@ -779,6 +956,17 @@ def dry_run(args, rank, world):
     elapsed = timed_steps(lambda i: time.sleep(0.01), args.steps, lambda: None,
                           dist.barrier if distributed else None)
     elapsed_max = max_over_ranks(elapsed)
+    bs = args.block_size
+    oracle_lib = load_oracle()
+    buf = np.empty(count * bs // 8, dtype=np.uint64)
+    oracle_lib.oracle_splitmix64_fill(buf.ctypes.data, 0, buf.size, SEED_C4, bs // 8, first)
+    digests = np.empty(count * 32, dtype=np.uint8)
+    oracle_lib.oracle_hash_chunks(buf.ctypes.data, count * bs, bs, digests.ctypes.data, 1)
+    if rank == args.dry_run_bad_rank:
+        digests[32 * (count - 1)] ^= 1  # the shard's last block: a range boundary
+    nbad, checked = config4_check(oracle_lib, digests, count * bs, bs, first, sample=8)
+    rows = job_summary([nbad, checked, 0, 10.0 + rank, 10.0 + rank])
+    parity, checked_all = job_parity(rows)
     bounds = torch.tensor([first, count], dtype=torch.int64)
     parts = [torch.zeros_like(bounds) for _ in range(world)]
     if distributed:
@@ -792,18 +980,22 @@ def dry_run(args, rank, world):
             "steps": args.steps, "ms_per_step": round(elapsed_max / max(1, args.steps) * 1e3, 4),
             "config": {"workload": "config4" if distributed else "config2",
                        "blocks_per_gpu": args.blocks, "block_size": args.block_size},
+            "parity": parity, "parity_checked_blocks": checked_all,
+            "per_rank": [{"rank": i, "mismatches": int(r[0]), "checked": int(r[1]),
+                          "kernel_ms_avg": r[3]} for i, r in enumerate(rows)],
             "shards": [p.tolist() for p in parts]}), flush=True)
     if distributed:
         dist.destroy_process_group()
-    return 0
+    return 0 if parity == "ok" else 1
 
 
 def main():
     args = parse()
-    # --gpus N > 1 with no launcher: spawn the ranks before anything touches a
-    # GPU (no torch.cuda call has run in this process yet; never exec)
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        return launch_ranks(args.gpus, sys.argv[1:])
+    # --gpus N > 1 (or --force-dist) with no launcher: spawn the ranks before
+    # anything touches a GPU (no torch.cuda call has run in this process yet;
+    # never exec)
+    if (args.gpus > 1 or args.force_dist) and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(max(1, args.gpus), sys.argv[1:])
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -830,6 +1022,9 @@ def main():
     torch.cuda.set_device(local % ndev)
     dev = torch.device("cuda", local % ndev)
     distributed = world > 1 or args.force_dist
+    # the process group's collectives (barrier, max-over-ranks, the job
+    # summary) run on this rank's GPU for RCCL, in host memory for gloo
+    coll_dev = dev if distributed and args.dist_backend == "nccl" else None
     if distributed:
         # RCCL prints its version banner on stdout when the communicator
         # comes up; keep stdout for the one JSON line (fd-level, so the C
@@ -853,7 +1048,9 @@ def main():
     nbytes = nblk * bs
     stream = torch.cuda.current_stream().cuda_stream
     t0 = time.perf_counter()
-    ctx = ca.Context(device_mask=1 << (local % ndev), staging_bytes=args.staging_mib << 20)
+    # the N>1 line hashes device-resident shards only: no staging slots
+    staging = ca._n.CIR_STAGING_LAZY if distributed else args.staging_mib << 20
+    ctx = ca.Context(device_mask=1 << (local % ndev), staging_bytes=staging)
     ctx_init_s = time.perf_counter() - t0
 
     if args.workload != "auto":
@@ -906,39 +1103,45 @@ def main():
     elapsed = timed_steps(timed_step, args.steps, torch.cuda.synchronize,
                           dist.barrier if distributed else None)
     kern_ms = [a.elapsed_time(b) for a, b in ev]
-    elapsed_max = max_over_ranks(elapsed, dev if args.dist_backend == "nccl" else None)
+    elapsed_max = max_over_ranks(elapsed, coll_dev)
 
-    # parity spot checks (no oracle here: golden digests + step-to-step identity)
-    parity = "ok"
+    # parity, per rank (no oracle on the config-2 path: golden digests +
+    # step-to-step identity; config 4: sampled shard blocks vs the oracle),
+    # then reduced over the job so the line describes every rank
+    failed, reasons, nbad, checked = 0, [], 0, 0
     if not torch.equal(out, ref_out):
-        parity = "FAIL: digests differ between steps"
+        failed, reasons = 1, ["digests differ between steps"]
     if workload == "config2" and nblk >= 32:
         with open(os.path.join(ROOT, "tests", "golden", "blake2b256_vectors.json")) as f:
             gold = json.load(f)["config2"]
         if bs == gold["block_size"]:
             d = out[:32 * 32].cpu().numpy().reshape(32, 32)
-            if any(d[i].tobytes().hex() != gold["zero_block"] for i in range(16)) or \
-               any(d[i].tobytes().hex() != gold["range_block"] for i in range(16, 32)):
-                parity = "FAIL: golden config-2 blocks differ"
-    c4_checked = None
+            want = [gold["zero_block"]] * 16 + [gold["range_block"]] * 16
+            nbad = sum(d[i].tobytes().hex() != want[i] for i in range(32))
+            checked = 32
+            if nbad:
+                reasons.append("golden config-2 blocks differ")
     if workload == "config4":
-        import numpy as np
         oracle_lib = load_oracle()
-        nbad, c4_checked = config4_check(oracle_lib, out.cpu().numpy(), nbytes, bs, first)
+        nbad, checked = config4_check(oracle_lib, out.cpu().numpy(), nbytes, bs, first)
         if nbad:
-            parity = "FAIL: %d of %d sampled config-4 digests differ from the oracle" % (
-                nbad, c4_checked)
-    if parity != "ok":
-        log("PARITY " + parity)
+            reasons.append("sampled config-4 digests differ from the oracle")
+    if nbad or failed:
+        log("PARITY rank %d: %d of %d differ; %s" % (rank, nbad, checked, "; ".join(reasons)))
+    rows = job_summary([nbad, checked, failed, sum(kern_ms) / len(kern_ms), min(kern_ms)],
+                       coll_dev)
+    parity, checked_all = job_parity(rows, "; ".join(reasons) if rank == 0 else None)
     valu_ms = valu_ceiling(ca, nblk, bs, stream)
 
     if rank == 0:
-        avg_kern_s = sum(kern_ms) / len(kern_ms) / 1e3
+        # the roofline of the job's slowest rank: its average launch time
+        slow = max(range(len(rows)), key=lambda i: rows[i][3])
+        avg_kern_s = rows[slow][3] / 1e3
         algo_bytes = nbytes + 32 * nblk
         achieved = algo_bytes / avg_kern_s / 1e9
-        loader_name = "glds" if args.loader in ("api", "glds") else "direct"
+        ep = entry_point(args.loader)
         # traffic depends on the launch shape, not on the bytes' values
-        cfg_key = "bs%d/n%d/%s" % (bs, nblk, loader_name)
+        cfg_key = traffic_key(bs, nblk, args.loader)
         traffic = load_traffic(cfg_key)
         cycles = load_traffic(cfg_key, "cycles")
         rec = {
@@ -957,7 +1160,8 @@ def main():
             "config": {
                 "workload": "%s: %d x %d B blocks per GPU (%.0f GiB), splitmix64, device-resident"
                             % (workload, nblk, bs, nbytes / GIB),
-                "blocks_per_gpu": nblk, "block_size": bs, "loader": loader_name,
+                "blocks_per_gpu": nblk, "block_size": bs,
+                "entry_point": ep["entry_point"], "loader": ep["loader"],
                 "parallelism": "range-split x%d, no collective" % world,
             },
             "roofline": {
@@ -965,9 +1169,12 @@ def main():
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "kernel_ms_avg": round(avg_kern_s * 1e3, 4),
-                "kernel_ms_min": round(min(kern_ms), 4),
+                "kernel_ms_min": round(min(r[4] for r in rows), 4),
+                "kernel_rank": slow,
+                "kernel_ms_avg_per_rank": [round(r[3], 4) for r in rows],
                 # SURVEY.md 8d quotes the median of >= 10 HIP-event timed runs
-                "kernel_ms_median": round(sorted(kern_ms)[len(kern_ms) // 2], 4),
+                # (rank 0's launches)
+                "kernel_ms_median_rank0": round(sorted(kern_ms)[len(kern_ms) // 2], 4),
                 "valu_ceiling_ms": valu_ms,
                 "valu_frac": round(valu_ms / (avg_kern_s * 1e3), 4) if valu_ms else None,
                 # from the committed PMC pass (profiles/pmc_traffic.json): the
@@ -977,7 +1184,8 @@ def main():
                 "clock_ghz": ({"kernel": cycles["clock_ghz_k_chunks"],
                                "register_only": cycles["clock_ghz_k_compress_only"]}
                               if cycles else None),
-                "note": "binding roof is integer VALU (~2.0k VALU ops per 128-B "
+                "note": "achieved and kernel_ms_avg are the slowest rank's (kernel_rank); "
+                        "binding roof is integer VALU (~2.0k VALU ops per 128-B "
                         "compression): valu_ceiling_ms = the same number of "
                         "compressions in registers with no memory traffic, timed "
                         "live; valu_frac = valu_ceiling_ms / kernel_ms_avg; cycle_frac "
@@ -986,13 +1194,12 @@ def main():
                         "the clock); see DESIGN.md 4.1",
             },
             "parity": parity,
+            "parity_checked_blocks": checked_all,
         }
         if distributed:
             # the process group's own count: every rank of the job took part
             rec["ranks_seen"] = dist.get_world_size()
             rec["dist_backend"] = args.dist_backend
-        if c4_checked:
-            rec["parity_checked_blocks"] = c4_checked
         if ranks_per_gpu > 1:
             rec["config"]["ranks_per_gpu"] = ranks_per_gpu
         if not distributed and not args.no_cpu_baseline:

@@ -192,6 +192,38 @@ class Context:
                                     ctypes.byref(ln)))
         return _n.take_buffer(out.value, ln.value)
 
+    # ---- footer placement and scan timing (diagnostics) -------------------
+    FOOTER_HOST, FOOTER_GPU = 0, 1
+    SCAN_BATCH_FIELDS = ("device", "bytes", "blocks", "wait_ms", "read_start_ms", "read_end_ms",
+                         "h2d_start_ms", "h2d_end_ms", "hash_start_ms", "done_ms")
+    SCAN_PHASE_FIELDS = ("walk_ms", "hash_loop_ms", "last_emit_ms", "footer_tail_ms",
+                         "output_ms", "footer_busy_ms", "footer_mode", "batches", "index_bytes",
+                         "footer_feeds")
+
+    def set_footer_mode(self, mode):
+        """Where cir_scan_v1 hashes a blake2b/256 footer: FOOTER_HOST (one host
+        thread beside the scan, the default) or FOOTER_GPU (the chain kernel)."""
+        _n.check(_n.lib.cir_set_footer_mode(self._h, mode))
+
+    def scan_timing(self, enable=True):
+        _n.check(_n.lib.cir_debug_scan_timing(self._h, 1 if enable else 0))
+
+    def scan_batches(self):
+        """One dict per staged batch of the scans since scan_timing(True)."""
+        n = ctypes.c_size_t()
+        _n.check(_n.lib.cir_debug_scan_batches(self._h, None, 0, ctypes.byref(n)))
+        k = len(self.SCAN_BATCH_FIELDS)
+        rows = (ctypes.c_double * (k * max(1, n.value)))()
+        _n.check(_n.lib.cir_debug_scan_batches(self._h, rows, n.value, ctypes.byref(n)))
+        return [dict(zip(self.SCAN_BATCH_FIELDS, rows[i * k:(i + 1) * k]))
+                for i in range(n.value)]
+
+    def scan_phases(self):
+        """The phase record of the last scan since scan_timing(True)."""
+        out = (ctypes.c_double * len(self.SCAN_PHASE_FIELDS))()
+        _n.check(_n.lib.cir_debug_scan_phases(self._h, out))
+        return dict(zip(self.SCAN_PHASE_FIELDS, list(out)))
+
     def index_rewrite(self, data):
         ptr, keep = _buf(data)
         out = ctypes.c_void_p()

@@ -43,6 +43,7 @@ CIR_ENOTFOUND = -6
 CIR_EHASHSIZE = -7
 CIR_ENODEV = -8
 CIR_EUNSUPPORTED = -9
+CIR_STAGING_LAZY = (1 << 64) - 1  # cir_init: no staging slots until a host path needs them
 
 CIR_HASH_BLAKE2B_256 = 1
 CIR_HASH_SHA512_256 = 2
@@ -105,6 +106,12 @@ _SIGS = {
     "cir_debug_relay_blocks": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint64]),
     "cir_debug_desc_timing": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "cir_debug_desc_times": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double)]),
+    "cir_set_footer_mode": (ctypes.c_int, [c_vp, ctypes.c_int]),
+    "cir_debug_scan_timing": (ctypes.c_int, [c_vp, ctypes.c_int]),
+    "cir_debug_scan_batches": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double),
+                                              ctypes.c_size_t, c_sizep]),
+    "cir_debug_scan_phases": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double)]),
+    "cir_debug_host_blake2b256": (ctypes.c_int, [c_vp, ctypes.c_size_t, ctypes.c_size_t, c_vp]),
     "cir_debug_hash_uniform_dev": (ctypes.c_int, [ctypes.c_int, c_vp, ctypes.c_uint64,
                                                   ctypes.c_uint64, c_vp, c_vp]),
     "cir_fill_splitmix64_dev": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint64,

@@ -17,6 +17,7 @@
 #include <dirent.h>
 #include <fcntl.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -50,18 +51,24 @@ static int die(int rc, const char* what) {
   return rc == CIR_EIO ? 1 : 2;
 }
 
-// Bytes of the regular files under path (symlinks not followed, as the scan
-// does), counted only until they reach cap.
-static uint64_t tree_bytes(const std::string& path, uint64_t cap, uint64_t acc = 0) {
+// Bytes of the regular files under path, counted only until they reach cap.
+// The top-level argument is followed as the scan and the hash path follow it
+// (opendir / open): a symlinked SRC or FILE counts its target; entries inside
+// directories are not followed (lstat), as walk() does.  A top-level argument
+// that is neither a regular file nor a directory (a pipe, /dev/stdin) has no
+// size to count and gets the default staging (returns cap).
+static uint64_t tree_bytes(const std::string& path, uint64_t cap, uint64_t acc = 0,
+                           bool top = true) {
   struct stat st;
-  if (acc >= cap || lstat(path.c_str(), &st) != 0) return acc;
+  if (acc >= cap) return acc;
+  if ((top ? stat(path.c_str(), &st) : lstat(path.c_str(), &st)) != 0) return top ? cap : acc;
   if (S_ISREG(st.st_mode)) return acc + (uint64_t)st.st_size;
-  if (!S_ISDIR(st.st_mode)) return acc;
+  if (!S_ISDIR(st.st_mode)) return top ? cap : acc;
   DIR* d = opendir(path.c_str());
   if (!d) return acc;
   while (struct dirent* e = readdir(d)) {
     if (!strcmp(e->d_name, ".") || !strcmp(e->d_name, "..")) continue;
-    acc = tree_bytes(path + "/" + e->d_name, cap, acc);
+    acc = tree_bytes(path + "/" + e->d_name, cap, acc, false);
     if (acc >= cap) break;
   }
   closedir(d);
@@ -141,7 +148,12 @@ int main(int argc, char** argv) {
   std::vector<std::string> inputs = files;
   for (const Job& j : jobs) inputs.push_back(j.src);
   cir_ctx* ctx = nullptr;
-  int rc = cir_init(&ctx, 0, staging_for(inputs));
+  const uint64_t staging = staging_for(inputs);
+  if (const char* t = getenv("CIR_TRACE"))
+    if (*t && strcmp(t, "0") != 0)
+      fprintf(stderr, "ciruela-index: staging %llu bytes per slot (0 = library default)\n",
+              (unsigned long long)staging);
+  int rc = cir_init(&ctx, 0, staging);
   if (rc) return die(rc, "cir_init");
   if (cmd == "hash") {
     for (const std::string& f : files) {

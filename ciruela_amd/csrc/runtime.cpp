@@ -46,9 +46,10 @@ Device::~Device() {
     (void)hipFree(s.d_out);
     if (s.copied) (void)hipEventDestroy(s.copied);
     if (s.done) (void)hipEventDestroy(s.done);
-    for (hipEvent_t e : {s.t_copy0, s.t_copy1, s.t_hash0})
+    for (hipEvent_t e : {s.t_copy0, s.t_copy1, s.t_hash0, s.t_done})
       if (e) (void)hipEventDestroy(e);
   }
+  if (t_ref) (void)hipEventDestroy(t_ref);
   if (chain) (void)hipStreamSynchronize(chain);
   for (int k = 0; k < 2; ++k) {
     (void)hipHostFree(chain_h[k]);
@@ -125,12 +126,7 @@ unsigned host_copy_threads() {
 int Device::ensure_slot(Slot& s, uint64_t bytes, uint64_t nblk) {
   if (!s.copied) {
     CIR_HIP(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
-    CIR_HIP(hipEventCreateWithFlags(&s.done, trace_enabled() ? 0 : hipEventDisableTiming));
-    if (trace_enabled()) {
-      CIR_HIP(hipEventCreate(&s.t_copy0));
-      CIR_HIP(hipEventCreate(&s.t_copy1));
-      CIR_HIP(hipEventCreate(&s.t_hash0));
-    }
+    CIR_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
   }
   const auto t0 = std::chrono::steady_clock::now();
   bool grew = false;
@@ -176,6 +172,13 @@ int Device::ensure_slot(Slot& s, uint64_t bytes, uint64_t nblk) {
             (int)(&s - slot), s.cap / 1048576.0, (unsigned long long)s.cap_blk,
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0)
                 .count());
+  return CIR_OK;
+}
+
+int Device::ensure_timing(Slot& s) {
+  for (hipEvent_t* e : {&s.t_copy0, &s.t_copy1, &s.t_hash0, &s.t_done})
+    if (!*e) CIR_HIP(hipEventCreate(e));
+  if (!t_ref) CIR_HIP(hipEventCreate(&t_ref));
   return CIR_OK;
 }
 
@@ -269,6 +272,8 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
   // diagnostics: a fresh event set per batch while timing is on (at most
   // kMaxTimedBatches per enable)
   constexpr size_t kMaxTimedBatches = 256;
+  // (the set counts as recorded only once every event of it is: a batch that
+  // fails part-way leaves it to the next batch)
   const hipEvent_t* tev = nullptr;
   if (d.timing && ht != CIR_HASH_SHA512_256 && d.tev_used < kMaxTimedBatches) {
     if (d.tev_used == d.tev.size()) {
@@ -276,7 +281,7 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
       for (hipEvent_t& e : set) CIR_HIP(hipEventCreate(&e));
       d.tev.push_back(set);
     }
-    tev = d.tev[d.tev_used++].data();
+    tev = d.tev[d.tev_used].data();
     CIR_HIP(hipEventRecord(tev[0], s));
   }
   uint32_t* perm = nullptr;
@@ -290,6 +295,7 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
                               d.part_fork, d.q_join,
                               d.relay_mem ? &d.relay : nullptr, tev ? tev + 2 : nullptr));
   CIR_HIP(hipEventRecord(d.order_free, s));
+  if (tev) ++d.tev_used;
   return CIR_OK;
 }
 
@@ -298,17 +304,22 @@ int hash_desc_ordered(Device& d, const uint8_t* arena, const uint64_t* off, cons
 // bytes of one file split into chunk_bs blocks (nblk = ceil(bytes / bs)).
 static int slot_submit_impl(Device& d, Slot& s, uint64_t bytes, uint64_t nblk,
                             uint64_t chunk_bs, int ht) {
-  if (s.t_copy0) CIR_HIP(hipEventRecord(s.t_copy0, d.copy));
+  s.timed = d.record_times || trace_enabled();
+  if (s.timed) {
+    int rc = d.ensure_timing(s);
+    if (rc) return rc;
+    CIR_HIP(hipEventRecord(s.t_copy0, d.copy));
+  }
   const uint8_t* src = s.d_data;
   CIR_HIP(hipMemcpyAsync(s.d_data, s.h_data, bytes, hipMemcpyHostToDevice, d.copy));
   if (chunk_bs == 0) {
     CIR_HIP(hipMemcpyAsync(s.d_off, s.h_off, nblk * 8, hipMemcpyHostToDevice, d.copy));
     CIR_HIP(hipMemcpyAsync(s.d_len, s.h_len, nblk * 4, hipMemcpyHostToDevice, d.copy));
   }
-  if (s.t_copy1) CIR_HIP(hipEventRecord(s.t_copy1, d.copy));
+  if (s.timed) CIR_HIP(hipEventRecord(s.t_copy1, d.copy));
   CIR_HIP(hipEventRecord(s.copied, d.copy));
   CIR_HIP(hipStreamWaitEvent(d.compute, s.copied, 0));
-  if (s.t_hash0) CIR_HIP(hipEventRecord(s.t_hash0, d.compute));
+  if (s.timed) CIR_HIP(hipEventRecord(s.t_hash0, d.compute));
   if (chunk_bs == 0) {
     int rc = hash_desc_ordered(d, src, s.d_off, s.d_len, nblk, s.d_out, d.compute, ht);
     if (rc) return rc;
@@ -316,6 +327,7 @@ static int slot_submit_impl(Device& d, Slot& s, uint64_t bytes, uint64_t nblk,
     CIR_HIP(dev::launch_chunks(src, bytes, chunk_bs, s.d_out, d.compute));
   CIR_HIP(hipMemcpyAsync(s.h_out, s.d_out, nblk * 32, hipMemcpyDeviceToHost, d.compute));
   CIR_HIP(hipEventRecord(s.done, d.compute));
+  if (s.timed) CIR_HIP(hipEventRecord(s.t_done, d.compute));
   s.busy = true;
   return CIR_OK;
 }
@@ -600,13 +612,15 @@ static int export_hashes(const std::vector<uint8_t>& h, uint8_t** out, size_t* n
 //   * the staging, part and footer-chain streams, their events and the relay
 //     scratch (zeroed with one synchronised memset);
 //   * the three staging slots at the context's staging size (pinned host +
-//     device buffers, descriptor and digest buffers for a full batch) and
-//     the ordering scratch for one such batch;
+//     device buffers, descriptor and digest buffers for a full batch) -- or,
+//     with `lazy` (CIR_STAGING_LAZY), two 64 KiB slots for the warm-up only,
+//     grown by the first host-path call -- and the ordering scratch for one
+//     full batch;
 //   * one tiny chunk-form hash and one ordered descriptor batch on the
 //     compute stream, which load the code object and touch every buffer;
-//   * one 4 MiB upload on the staging and on the footer-chain stream.
+//   * one small upload on the staging and on the footer-chain stream.
 // Caller holds a DeviceGuard.
-static int init_device(Device& d, uint64_t staging) {
+static int init_device(Device& d, uint64_t staging, bool lazy) {
   CIR_HIP(hipSetDevice(d.id));
   CIR_HIP(hipStreamCreateWithFlags(&d.compute, hipStreamNonBlocking));
   CIR_HIP(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
@@ -621,8 +635,9 @@ static int init_device(Device& d, uint64_t staging) {
     if (rc) return rc;
   }
   const uint64_t cap_blk = std::max<uint64_t>(staging / 512, 4096);
-  for (Slot& s : d.slot) {
-    const int rc = d.ensure_slot(s, std::max<uint64_t>(staging, 16), cap_blk);
+  const uint64_t slot_bytes = lazy ? (64ull << 10) : std::max<uint64_t>(staging, 16);
+  for (int k = 0; k < (lazy ? 2 : Device::kSlots); ++k) {
+    const int rc = d.ensure_slot(d.slot[k], slot_bytes, lazy ? 4096 : cap_blk);
     if (rc) return rc;
   }
   Slot& s = d.slot[0];
@@ -638,12 +653,33 @@ static int init_device(Device& d, uint64_t staging) {
   // than the next (profiles/r03_s2/cli/: a 10 MiB batch's upload 7.7-10.7 ms
   // in a fresh CLI process, ~0.2 ms later): pay it here for the staging and
   // footer-chain streams, with copies big enough to take the DMA engine path
-  const size_t warm = (size_t)std::min<uint64_t>(staging, 4ull << 20);
+  const size_t warm = (size_t)std::min<uint64_t>(slot_bytes, 4ull << 20);
   CIR_HIP(hipMemcpyAsync(s.d_data, s.h_data, warm, hipMemcpyHostToDevice, d.copy));
   CIR_HIP(hipMemcpyAsync(d.slot[1].d_data, d.slot[1].h_data, warm, hipMemcpyHostToDevice,
                          d.chain));
   CIR_HIP(hipStreamSynchronize(d.copy));
   CIR_HIP(hipStreamSynchronize(d.chain));
+  return CIR_OK;
+}
+
+// Open the given devices, one host thread each (a device's warm-up waits on
+// its own streams only); the first failure in device order is returned.
+static int init_devices(std::vector<std::unique_ptr<Device>>& devs, uint64_t staging, bool lazy) {
+  if (devs.size() == 1) {
+    DeviceGuard guard;
+    return init_device(*devs[0], staging, lazy);
+  }
+  std::vector<int> rc(devs.size(), 0);
+  std::vector<std::string> err(devs.size());
+  std::vector<std::thread> th;
+  for (size_t i = 0; i < devs.size(); ++i)
+    th.emplace_back([&, i] {
+      rc[i] = init_device(*devs[i], staging, lazy);
+      if (rc[i]) err[i] = t_last_error;
+    });
+  for (auto& t : th) t.join();
+  for (size_t i = 0; i < devs.size(); ++i)
+    if (rc[i]) return fail(rc[i], err[i]);
   return CIR_OK;
 }
 
@@ -685,15 +721,14 @@ int cir_init(cir_ctx** out, uint32_t device_mask, uint64_t staging_bytes) {
     return fail(CIR_ENODEV, std::string("no HIP device: ") + hipGetErrorString(e));
   DeviceGuard guard;
   auto ctx = std::make_unique<cir_ctx>();
-  ctx->staging = staging_bytes ? staging_bytes : (256ull << 20);
+  const bool lazy = staging_bytes == CIR_STAGING_LAZY;
+  ctx->staging = staging_bytes && !lazy ? staging_bytes : (256ull << 20);
   for (int i = 0; i < n && i < 32; ++i) {
     if (device_mask && !(device_mask & (1u << i))) continue;
     int rc = check_device(i);
     if (rc) return rc;
     auto d = std::make_unique<Device>();
     d->id = i;
-    rc = init_device(*d, ctx->staging);
-    if (rc) return rc;
     ctx->devs.push_back(std::move(d));
   }
   if (ctx->devs.empty()) return fail(CIR_ENODEV, "device_mask selects no visible device");
@@ -707,11 +742,13 @@ int cir_init(cir_ctx** out, uint32_t device_mask, uint64_t staging_bytes) {
       for (size_t i = 0; i < n0; ++i) {
         auto d = std::make_unique<Device>();
         d->id = ctx->devs[i]->id;
-        const int rc = init_device(*d, ctx->staging);
-        if (rc) return rc;
         ctx->devs.push_back(std::move(d));
       }
   }
+  int rc = init_devices(ctx->devs, ctx->staging, lazy);
+  if (rc) return rc;
+  if (const char* v = std::getenv("CIR_FOOTER"))
+    ctx->footer = strcmp(v, "gpu") == 0 ? CIR_FOOTER_GPU : CIR_FOOTER_HOST;
   *out = ctx.release();
   return CIR_OK;
 }

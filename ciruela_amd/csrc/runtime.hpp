@@ -60,8 +60,10 @@ struct Slot {
   uint64_t cap_blk = 0;
   hipEvent_t copied = nullptr;  // H2D of this slot finished (copy stream)
   hipEvent_t done = nullptr;    // digests of this slot are back in h_out
-  // timing events, recorded only when CIR_TRACE is set (trace_enabled())
-  hipEvent_t t_copy0 = nullptr, t_copy1 = nullptr, t_hash0 = nullptr;
+  // timing events (created on first use, recorded only while the device's
+  // record_times is set: CIR_TRACE, or cir_debug_scan_timing during a scan)
+  hipEvent_t t_copy0 = nullptr, t_copy1 = nullptr, t_hash0 = nullptr, t_done = nullptr;
+  bool timed = false;  // this slot's last submit recorded them
   bool busy = false;
 };
 
@@ -81,6 +83,9 @@ struct Device {
   int id = 0;
   hipStream_t compute = nullptr;
   hipStream_t copy = nullptr;
+  // per-batch timing of the staged path (slot_submit records t_* events)
+  bool record_times = false;
+  hipEvent_t t_ref = nullptr;  // a scan's time origin on the copy stream
   // staging slots: the batch entry points cycle through two; the directory
   // scan through all three (reads of batch k+1 overlap the H2D of k and k-1).
   static constexpr int kSlots = 3;
@@ -125,6 +130,7 @@ struct Device {
   size_t tev_used = 0;
   ~Device();
   int ensure_slot(Slot& s, uint64_t bytes, uint64_t nblk);
+  int ensure_timing(Slot& s);
 };
 
 // A batch of blocks already packed in a slot's host buffer:
@@ -140,9 +146,30 @@ int slot_wait(Device& d, Slot& s);
 
 }  // namespace cir
 
+namespace cir {
+// cir_debug_scan_timing: one row per staged batch of the last scans, one
+// phase record per scan (fields: include/ciruela_blockhash.h)
+constexpr int kScanBatchFields = 10;
+constexpr int kScanPhaseFields = 10;
+static_assert(kScanBatchFields == CIR_SCAN_BATCH_FIELDS && kScanPhaseFields == CIR_SCAN_PHASE_FIELDS,
+              "scan stats layout");
+struct ScanStats {
+  std::mutex mu;
+  bool on = false;
+  std::vector<std::array<double, kScanBatchFields>> batches;
+  std::array<double, kScanPhaseFields> phases{};
+  size_t scans = 0;
+};
+}  // namespace cir
+
 struct cir_ctx {
   std::vector<std::unique_ptr<cir::Device>> devs;
   uint64_t staging = 0;
+  // where cir_scan_v1 hashes a blake2b/256 index's footer: CIR_FOOTER_HOST
+  // (one host thread beside the scan) or CIR_FOOTER_GPU (the resumable
+  // single-chain kernel on device 0's chain stream)
+  int footer = CIR_FOOTER_HOST;
+  cir::ScanStats stats;
 };
 
 namespace cir {

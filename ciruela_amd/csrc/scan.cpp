@@ -23,12 +23,14 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdlib>
 #include <map>
 #include <memory>
 #include <functional>
 #include <thread>
 
+#include "blake2b_host.hpp"
 #include "dirsig.hpp"
 #include "runtime.hpp"
 
@@ -179,12 +181,30 @@ using Progress = std::function<int(uint64_t done_blk)>;
 // order; a range may start or end inside a file).  done(n) is called after
 // each batch with the number of blocks of the range finished so far (a
 // prefix of the range: the slots retire in submission order).
-static int hash_range(cir_ctx* ctx, Device& d, const std::vector<ScanFile>& files, uint64_t bs,
-                      unsigned threads, int ht, std::vector<uint8_t>& digests, uint64_t b0,
-                      uint64_t b1, const std::function<int(uint64_t)>& done) {
+// With `scan_t0` >= 0 (cir_debug_scan_timing on) every batch is timed and
+// appended to ctx->stats as a row (include/ciruela_blockhash.h), times in ms
+// since scan_t0 on the host clock; the device's copy stream gets a reference
+// event at the start that maps its HIP event times onto that clock.
+static int hash_range(cir_ctx* ctx, Device& d, size_t di, const std::vector<ScanFile>& files,
+                      uint64_t bs, unsigned threads, int ht, std::vector<uint8_t>& digests,
+                      uint64_t b0, uint64_t b1, const std::function<int(uint64_t)>& done,
+                      double scan_t0) {
   std::lock_guard<std::mutex> lk(d.mu);
   DeviceGuard guard;
   CIR_HIP(hipSetDevice(d.id));
+  const bool stats = scan_t0 >= 0;
+  struct RecordTimes {  // the device's slots are timed for this range only
+    Device& d;
+    ~RecordTimes() { d.record_times = false; }
+  } record_times{d};
+  d.record_times = stats;
+  double ref_ms = 0;  // host time of the copy stream's reference event
+  if (stats) {
+    if (!d.t_ref) CIR_HIP(hipEventCreate(&d.t_ref));
+    CIR_HIP(hipEventRecord(d.t_ref, d.copy));
+    ref_ms = now_ms() - scan_t0;
+  }
+  std::vector<std::array<double, kScanBatchFields>> rows;
   const uint64_t cap = std::max<uint64_t>(ctx->staging, bs + 16);
   const uint64_t cap_blk = std::max<uint64_t>(cap / 512, 4096);
   // first file with a block >= b0
@@ -195,6 +215,7 @@ static int hash_range(cir_ctx* ctx, Device& d, const std::vector<ScanFile>& file
   uint64_t fblk = b0 > files[fi].first_blk ? b0 - files[fi].first_blk : 0;  // next block within it
   constexpr int kS = Device::kSlots;
   uint64_t pending_first[kS] = {}, pending_n[kS] = {};
+  double pending_row[kS][6] = {};  // bytes, blocks, wait, read start, read end
   int k = 0;
   auto busy = [&] {
     for (const Slot& s : d.slot)
@@ -210,23 +231,33 @@ static int hash_range(cir_ctx* ctx, Device& d, const std::vector<ScanFile>& file
   };
   while (more() || busy()) {
     Slot& s = d.slot[k];
-    const double t_wait0 = trace_on() ? now_ms() : 0;
+    const double t_wait0 = (trace_on() || stats) ? now_ms() : 0;
     if (s.busy) {
+      const bool timed = s.timed;
       int rc = slot_wait(d, s);
       if (rc) return rc;
-      if (trace_on() && s.t_copy0) {
+      if (timed && trace_on()) {
         float copy_ms = 0, hash_ms = 0, gap_ms = 0;
         (void)hipEventElapsedTime(&copy_ms, s.t_copy0, s.t_copy1);
         (void)hipEventElapsedTime(&gap_ms, s.t_copy1, s.t_hash0);
-        (void)hipEventElapsedTime(&hash_ms, s.t_hash0, s.done);
+        (void)hipEventElapsedTime(&hash_ms, s.t_hash0, s.t_done);
         fprintf(stderr, "cir_scan dev %d slot %d: h2d %.2f ms, h2d->hash %.2f ms, hash+d2h %.2f ms\n",
                 d.id, k, copy_ms, gap_ms, hash_ms);
+      }
+      if (timed && stats) {
+        float e[4] = {0, 0, 0, 0};
+        const hipEvent_t ev[4] = {s.t_copy0, s.t_copy1, s.t_hash0, s.t_done};
+        for (int j = 0; j < 4; ++j) CIR_HIP(hipEventElapsedTime(&e[j], d.t_ref, ev[j]));
+        rows.push_back({(double)di, pending_row[k][0], pending_row[k][1], pending_row[k][2],
+                        pending_row[k][3], pending_row[k][4], ref_ms + e[0], ref_ms + e[1],
+                        ref_ms + e[2], ref_ms + e[3]});
       }
       memcpy(digests.data() + 32 * pending_first[k], s.h_out, 32 * pending_n[k]);
       rc = done(pending_first[k] + pending_n[k] - b0);
       if (rc) return rc;
     }
-    const double t_wait1 = trace_on() ? now_ms() : 0;
+    const bool clock = trace_on() || stats;
+    const double t_wait1 = clock ? now_ms() : 0;
     if (more()) {
       int rc = d.ensure_slot(s, cap, cap_blk);
       if (rc) return rc;
@@ -256,10 +287,10 @@ static int hash_range(cir_ctx* ctx, Device& d, const std::vector<ScanFile>& file
         n += take;
         fblk += take;
       }
-      const double t_read0 = trace_on() ? now_ms() : 0;
+      const double t_read0 = clock ? now_ms() : 0;
       rc = run_reads(jobs, files, threads);
       if (rc) return rc;
-      const double t_read1 = trace_on() ? now_ms() : 0;
+      const double t_read1 = clock ? now_ms() : 0;
       rc = slot_submit(d, s, std::max<uint64_t>(pos, 16), n, ht);
       if (rc) return rc;
       if (trace_on())
@@ -268,8 +299,19 @@ static int hash_range(cir_ctx* ctx, Device& d, const std::vector<ScanFile>& file
                 pos / 1e6 / std::max(t_read1 - t_read0, 1e-3));
       pending_first[k] = first;
       pending_n[k] = n;
+      if (stats) {
+        pending_row[k][0] = (double)pos;
+        pending_row[k][1] = (double)n;
+        pending_row[k][2] = t_wait1 - t_wait0;
+        pending_row[k][3] = t_read0 - scan_t0;
+        pending_row[k][4] = t_read1 - scan_t0;
+      }
     }
     k = (k + 1) % kS;
+  }
+  if (stats) {
+    std::lock_guard<std::mutex> sl(ctx->stats.mu);
+    ctx->stats.batches.insert(ctx->stats.batches.end(), rows.begin(), rows.end());
   }
   return CIR_OK;
 }
@@ -284,7 +326,8 @@ static int hash_range(cir_ctx* ctx, Device& d, const std::vector<ScanFile>& file
 // global order that is complete, called under a lock on device 0's
 // current-device setting (the emitter feeds device 0's footer chain).
 static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, unsigned threads,
-                      int ht, std::vector<uint8_t>& digests, const Progress& progress) {
+                      int ht, std::vector<uint8_t>& digests, const Progress& progress,
+                      double scan_t0) {
   uint64_t nblk_total = 0;
   for (ScanFile& f : files) {
     f.first_blk = nblk_total;
@@ -294,7 +337,8 @@ static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, u
   if (nblk_total == 0) return CIR_OK;
   const size_t nd = std::min<size_t>(ctx->devs.size(), nblk_total);
   if (nd <= 1)
-    return hash_range(ctx, *ctx->devs[0], files, bs, threads, ht, digests, 0, nblk_total, progress);
+    return hash_range(ctx, *ctx->devs[0], 0, files, bs, threads, ht, digests, 0, nblk_total,
+                      progress, scan_t0);
   std::vector<uint64_t> lo(nd), hi(nd), got(nd, 0);
   for (size_t i = 0; i < nd; ++i) {
     lo[i] = nblk_total * i / nd;
@@ -323,8 +367,8 @@ static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, u
   std::vector<std::thread> th;
   for (size_t i = 0; i < nd; ++i)
     th.emplace_back([&, i] {
-      rc[i] = hash_range(ctx, *ctx->devs[i], files, bs, per, ht, digests, lo[i], hi[i],
-                         [&, i](uint64_t n) { return done(i, n); });
+      rc[i] = hash_range(ctx, *ctx->devs[i], i, files, bs, per, ht, digests, lo[i], hi[i],
+                         [&, i](uint64_t n) { return done(i, n); }, scan_t0);
       if (rc[i]) err[i] = cir_last_error();
     });
   for (auto& t : th) t.join();
@@ -346,7 +390,24 @@ struct FooterChain {
   Device& d;
   size_t fed = 0;
   int k = 0;
-  explicit FooterChain(Device& dev) : d(dev) {}
+  size_t feeds = 0;
+  // with `timed`, a pair of HIP events around every chain-step launch (the
+  // kernel only, not its text upload): busy_ms() sums them
+  bool timed = false;
+  std::vector<hipEvent_t> tev;
+  explicit FooterChain(Device& dev, bool t) : d(dev), timed(t) {}
+  ~FooterChain() {
+    if (!tev.empty()) (void)hipStreamSynchronize(d.chain);
+    for (hipEvent_t e : tev) (void)hipEventDestroy(e);
+  }
+  double busy_ms() {
+    double ms = 0;
+    for (size_t i = 0; i + 1 < tev.size(); i += 2) {
+      float x = 0;
+      if (hipEventElapsedTime(&x, tev[i], tev[i + 1]) == hipSuccess) ms += x;
+    }
+    return ms;
+  }
 
   int start() {
     if (!d.chain) {
@@ -385,8 +446,18 @@ struct FooterChain {
         memcpy(d.chain_h[k], body.data() + fed, piece);
         CIR_HIP(hipMemcpyAsync(d.chain_d[k], d.chain_h[k], piece, hipMemcpyHostToDevice, d.chain));
       }
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      if (timed) {
+        CIR_HIP(hipEventCreate(&e0));
+        tev.push_back(e0);
+        CIR_HIP(hipEventCreate(&e1));
+        tev.push_back(e1);
+        CIR_HIP(hipEventRecord(e0, d.chain));
+      }
       CIR_HIP(dev::launch_chain_step(d.chain_state, d.chain_d[k], (uint32_t)piece, last, d.chain));
+      if (timed) CIR_HIP(hipEventRecord(e1, d.chain));
       CIR_HIP(hipEventRecord(d.chain_done[k], d.chain));
+      ++feeds;
       k ^= 1;
       fed += piece;
       n -= piece;
@@ -410,6 +481,71 @@ struct FooterChain {
     CIR_HIP(hipStreamSynchronize(d.chain));
     return CIR_OK;
   }
+};
+
+// The same footer on one host thread (CIR_FOOTER_HOST, the default): every
+// completed stretch of the body is copied out (the emitter's string may grow
+// and move) and queued to a thread that feeds it to a streaming BLAKE2b-256
+// (blake2b_host.cpp), so hashing the ~106 MB of text of config 5 overlaps the
+// scan and the scan's tail after its last batch is the last stretch only.
+// Round 4, config 5 on one box (profiles/r04/footer/): see DESIGN.md 5.
+class HostFooter {
+ public:
+  HostFooter() : th_([this] { run(); }) {}
+  ~HostFooter() { close(); }
+  size_t fed() const { return fed_; }
+  size_t feeds() const { return feeds_; }
+  double busy_ms() const { return busy_ms_; }  // valid after finish()
+
+  void advance(const std::string& body, size_t min_feed) {
+    const size_t n = body.size() - fed_;
+    if (n == 0 || n < min_feed) return;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      q_.emplace_back(body, fed_, n);
+    }
+    cv_.notify_one();
+    fed_ += n;
+    ++feeds_;
+  }
+
+  void finish(const std::string& body, uint8_t out[32]) {
+    advance(body, 0);
+    close();
+    st_.final(out);
+  }
+
+ private:
+  void close() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      closed_ = true;
+    }
+    cv_.notify_one();
+    if (th_.joinable()) th_.join();
+  }
+  void run() {
+    for (;;) {
+      std::vector<std::string> take;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return closed_ || !q_.empty(); });
+        if (q_.empty()) return;  // closed and drained
+        take.swap(q_);
+      }
+      const double t0 = now_ms();
+      for (const std::string& c : take) st_.update((const uint8_t*)c.data(), c.size());
+      busy_ms_ += now_ms() - t0;
+    }
+  }
+  host::Blake2b256 st_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<std::string> q_;
+  bool closed_ = false;
+  size_t fed_ = 0, feeds_ = 0;
+  double busy_ms_ = 0;
+  std::thread th_;  // last: started once every other member exists
 };
 
 // ---- RawIndex::into_mut + MutableIndex::to_raw_data ---------------------
@@ -472,12 +608,22 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
     hdr.hash = dirsig::HashType::kSha512_256;
   else
     return fail(CIR_EINVAL, "unknown hash type");
-  // The incremental footer chain is BLAKE2b (quad mode); a sha512/256 footer
-  // is hashed once at the end (one lane).
+  // A blake2b/256 footer is hashed incrementally while the scan runs: on a
+  // host thread (CIR_FOOTER_HOST) or by the GPU chain kernel (CIR_FOOTER_GPU,
+  // quad mode); a sha512/256 footer is hashed once at the end (one lane).
   const bool incremental = hash_type == CIR_HASH_BLAKE2B_256;
+  const bool host_footer = incremental && ctx->footer == CIR_FOOTER_HOST;
+  const bool gpu_chain = incremental && !host_footer;
   if (threads == 0) threads = host_copy_threads();  // auto_threads
+  bool stats;
+  size_t rows0;  // this scan's batches are the rows recorded from here on
+  {
+    std::lock_guard<std::mutex> sl(ctx->stats.mu);
+    stats = ctx->stats.on;
+    rows0 = ctx->stats.batches.size();
+  }
 
-  const double t0 = trace_on() ? now_ms() : 0;
+  const double t0 = now_ms();
   std::vector<PlanItem> plan;
   std::vector<ScanFile> files;
   for (size_t i = 0; i < ndirs; ++i) {
@@ -489,16 +635,19 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
   }
   dirsig::Emitter em(hdr);
   Device& dv = *ctx->devs[0];
-  std::lock_guard<std::mutex> chain_lock(dv.chain_mu);
+  std::unique_lock<std::mutex> chain_lock(dv.chain_mu, std::defer_lock);
+  if (gpu_chain) chain_lock.lock();
   DeviceGuard guard;  // the caller's current device is restored on return
   CIR_HIP(hipSetDevice(dv.id));
-  FooterChain chain(dv);
-  int rc = incremental ? chain.start() : CIR_OK;
+  FooterChain chain(dv, stats);
+  std::unique_ptr<HostFooter> hfoot;
+  if (host_footer) hfoot = std::make_unique<HostFooter>();
+  int rc = gpu_chain ? chain.start() : CIR_OK;
   if (rc) return rc;
   std::vector<uint8_t> digests;
   size_t plan_pos = 0;
   // emit every plan item whose file blocks are all hashed (files complete in
-  // plan order), then feed the finished stretch of the body to the chain
+  // plan order), then feed the finished stretch of the body to the footer
   auto emit_ready = [&](uint64_t done_blk) -> int {
     for (; plan_pos < plan.size(); ++plan_pos) {
       const PlanItem& it = plan[plan_pos];
@@ -513,36 +662,55 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
         em.add_file(it.name, it.exe, f.size, digests.data() + 32 * f.first_blk, nb);
       }
     }
-    return incremental ? chain.advance(em.body(), (size_t)256 << 10) : (int)CIR_OK;
+    if (hfoot) hfoot->advance(em.body(), (size_t)256 << 10);
+    return gpu_chain ? chain.advance(em.body(), (size_t)256 << 10) : (int)CIR_OK;
   };
-  const double t1 = trace_on() ? now_ms() : 0;
-  rc = hash_files(ctx, files, block_size, threads, hash_type, digests, emit_ready);
+  const double t1 = now_ms();
+  rc = hash_files(ctx, files, block_size, threads, hash_type, digests, emit_ready,
+                  stats ? t0 : -1.0);
   if (rc) return rc;
-  const double t2 = trace_on() ? now_ms() : 0;
+  const double t2 = now_ms();
   rc = emit_ready(~0ull);
   if (rc) return rc;
-  const double t3 = trace_on() ? now_ms() : 0;
-  // Footer = H(every byte after the header line), finished on the GPU.
+  const double t3 = now_ms();
+  // Footer = H(every byte after the header line).
   const std::string& body = em.body();
-  if (body.size() - chain.fed > 0xffffffffull) return fail(CIR_EINVAL, "index tail above 4 GiB");
   uint8_t footer[32];
-  if (incremental) {
+  if (hfoot) {
+    hfoot->finish(body, footer);
+  } else if (gpu_chain) {
+    if (body.size() - chain.fed > 0xffffffffull) return fail(CIR_EINVAL, "index tail above 4 GiB");
     rc = chain.finish(body, footer);
   } else {
+    if (body.size() > 0xffffffffull) return fail(CIR_EINVAL, "index body longer than 4 GiB");
     const uint64_t off = 0;
     const uint32_t blen = (uint32_t)body.size();
     rc = cir_hash_blocks_ht(ctx, hash_type, (const uint8_t*)body.data(), &off, &blen, 1, footer);
   }
   if (rc) return rc;
-  const double t4 = trace_on() ? now_ms() : 0;
+  const double t4 = now_ms();
   *index_out = em.finish_malloc(footer, 32, len_out);
   if (!*index_out) return fail(CIR_ENOMEM, "malloc");
+  const double t5 = now_ms();
+  if (stats) {
+    std::lock_guard<std::mutex> sl(ctx->stats.mu);
+    ctx->stats.phases = {t1 - t0,
+                         t2 - t1,
+                         t3 - t2,
+                         t4 - t2,
+                         t5 - t4,
+                         hfoot ? hfoot->busy_ms() : gpu_chain ? chain.busy_ms() : 0.0,
+                         (double)(hfoot ? CIR_FOOTER_HOST : CIR_FOOTER_GPU),
+                         (double)(ctx->stats.batches.size() - rows0),
+                         (double)*len_out,
+                         (double)(hfoot ? hfoot->feeds() : chain.feeds)};
+    ++ctx->stats.scans;
+  }
   if (trace_on())
     fprintf(stderr,
             "cir_scan phases: walk %.1f ms, hash loop %.1f ms, last emit %.1f ms, footer %.1f ms, "
             "output %.1f ms; %zu files, index %.1f MiB\n",
-            t1 - t0, t2 - t1, t3 - t2, t4 - t3, now_ms() - t4, files.size(),
-            *len_out / 1048576.0);
+            t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4, files.size(), *len_out / 1048576.0);
   return CIR_OK;
 }
 
@@ -601,6 +769,51 @@ int cir_index_rewrite(cir_ctx* ctx, const uint8_t* in, size_t len, uint8_t** out
   if (rc) return rc;
   *out = em.finish_malloc(footer, 32, out_len);
   if (!*out) return fail(CIR_ENOMEM, "malloc");
+  return CIR_OK;
+}
+
+int cir_set_footer_mode(cir_ctx* ctx, int mode) {
+  if (!ctx) return fail(CIR_EINVAL, "null ctx");
+  if (mode != CIR_FOOTER_HOST && mode != CIR_FOOTER_GPU) return fail(CIR_EINVAL, "unknown footer mode");
+  ctx->footer = mode;
+  return CIR_OK;
+}
+
+int cir_debug_scan_timing(cir_ctx* ctx, int enable) {
+  if (!ctx) return fail(CIR_EINVAL, "null ctx");
+  std::lock_guard<std::mutex> sl(ctx->stats.mu);
+  ctx->stats.on = enable != 0;
+  if (enable) {
+    ctx->stats.batches.clear();
+    ctx->stats.phases.fill(0.0);
+    ctx->stats.scans = 0;
+  }
+  return CIR_OK;
+}
+
+int cir_debug_scan_batches(cir_ctx* ctx, double* rows, size_t max_rows, size_t* nrows) {
+  if (!ctx || !nrows || (max_rows && !rows)) return fail(CIR_EINVAL, "null pointer");
+  std::lock_guard<std::mutex> sl(ctx->stats.mu);
+  const auto& b = ctx->stats.batches;
+  for (size_t i = 0; i < b.size() && i < max_rows; ++i)
+    memcpy(rows + i * kScanBatchFields, b[i].data(), sizeof(double) * kScanBatchFields);
+  *nrows = b.size();
+  return CIR_OK;
+}
+
+int cir_debug_scan_phases(cir_ctx* ctx, double out[CIR_SCAN_PHASE_FIELDS]) {
+  if (!ctx || !out) return fail(CIR_EINVAL, "null pointer");
+  std::lock_guard<std::mutex> sl(ctx->stats.mu);
+  memcpy(out, ctx->stats.phases.data(), sizeof(double) * kScanPhaseFields);
+  return CIR_OK;
+}
+
+int cir_debug_host_blake2b256(const uint8_t* p, size_t n, size_t piece, uint8_t out[32]) {
+  if (!out || (n && !p)) return fail(CIR_EINVAL, "null pointer");
+  host::Blake2b256 h;
+  if (piece == 0) piece = n;
+  for (size_t off = 0; off < n; off += piece) h.update(p + off, std::min(piece, n - off));
+  h.final(out);
   return CIR_OK;
 }
 

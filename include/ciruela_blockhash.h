@@ -3,10 +3,11 @@
  *
  * Drop-in boundary for ciruela's indexing loop.  Every entry
  * point names the reference interface it replaces (paths are relative to the
- * tailhook/ciruela v0.6.12 tree).  All hashing runs on the GPU (hand-written
- * HIP kernels for gfx950); the host side stages bytes and bookkeeps.  There
- * is no CPU hashing fallback: without a usable GPU every hashing call returns
- * CIR_ENODEV.
+ * tailhook/ciruela v0.6.12 tree).  Every block digest is computed on the GPU
+ * (hand-written HIP kernels for gfx950); the host side stages bytes and
+ * bookkeeps, and by default hashes the one serial footer chain of a scanned
+ * index (cir_set_footer_mode).  There is no CPU fallback for block hashes:
+ * without a usable GPU every hashing call returns CIR_ENODEV.
  *
  * Conventions
  *   - return 0 (CIR_OK) on success, a negative CIR_E* code on failure; the
@@ -59,12 +60,21 @@ typedef struct cir_ctx cir_ctx;
 /* ---- context --------------------------------------------------------- */
 
 /* Open the devices in device_mask (bit i = HIP device i; 0 = every visible
- * device).  staging_bytes (0 = 256 MiB) sizes each device's host->device
- * staging slots for the host-memory entry points.  Everything a device
- * needs is created here -- streams, the relay scratch, three staging slots of
- * staging_bytes (pinned host + device memory each) -- and a tiny warm-up
- * hash loads the kernels, so no later call allocates or synchronises on the
- * device's behalf except to grow a buffer past these sizes. */
+ * device; the devices are opened in parallel, one host thread each).
+ * staging_bytes sizes each device's host->device staging slots for the
+ * host-memory entry points (0 = 256 MiB).  What cir_init creates per device:
+ * its streams (compute, copy, quad part, footer chain), the relay scratch,
+ * the ordering scratch for one full staging batch and -- unless staging_bytes
+ * is CIR_STAGING_LAZY -- three staging slots (pinned host + device memory of
+ * staging_bytes each, plus descriptor and digest buffers: about 3 x
+ * staging_bytes of pinned host memory and as much VRAM, 768 MiB each at the
+ * default).  A tiny warm-up hash loads the kernels and the first copies on the
+ * staging and chain streams are paid here.  Allocated later, on first use:
+ * the footer-chain text buffers (cir_scan_v1 with CIR_FOOTER_GPU), the
+ * single-launch buffers of cir_blake2b256, timing events, and -- with
+ * CIR_STAGING_LAZY -- the staging slots (256 MiB each), so a context used only
+ * through the *_dev entry points pins no staging memory. */
+#define CIR_STAGING_LAZY ((uint64_t)-1)
 int cir_init(cir_ctx** ctx, uint32_t device_mask, uint64_t staging_bytes);
 void cir_destroy(cir_ctx* ctx);
 int cir_device_count(void);
@@ -243,6 +253,41 @@ int cir_debug_compress_only_dev(uint64_t nlanes, uint32_t lines, uint8_t* d_out,
  * milliseconds, out[4] = summed ordering start -> last part end. */
 int cir_debug_desc_timing(cir_ctx* ctx, int enable);
 int cir_debug_desc_times(cir_ctx* ctx, double out[5]);
+
+/* Where cir_scan_v1 hashes the footer of a blake2b/256 index (the ImageId,
+ * H(every byte after the header line), src/index.rs:98-105): one serial
+ * chain over the index text, ~65 B per 32 KiB block.  CIR_FOOTER_HOST (the
+ * default): a host thread hashes the text as the scan emits it.
+ * CIR_FOOTER_GPU: the resumable single-chain kernel (quad mode) on device 0's
+ * chain stream.  Block digests are always computed on the GPU. */
+enum cir_footer_mode { CIR_FOOTER_HOST = 0, CIR_FOOTER_GPU = 1 };
+int cir_set_footer_mode(cir_ctx* ctx, int mode);
+
+/* Staged-scan timing of ctx (cir_scan_v1): enable != 0 clears the record and
+ * starts recording, 0 stops.  While on, every staged batch adds one row of
+ * CIR_SCAN_BATCH_FIELDS doubles:
+ *   [0] device index in ctx  [1] bytes  [2] blocks
+ *   [3] host wait for the slot (ms)
+ *   [4] reads start  [5] reads end            (ms since the scan started)
+ *   [6] H2D start    [7] H2D end              (HIP events on the copy stream)
+ *   [8] hash start   [9] digests back on host (HIP events, compute stream)
+ * and every scan sets CIR_SCAN_PHASE_FIELDS doubles:
+ *   [0] walk ms  [1] hash loop ms  [2] last emit ms
+ *   [3] footer tail ms (hash loop end -> footer digest)  [4] output ms
+ *   [5] footer busy ms (host thread hashing, or summed chain-kernel time)
+ *   [6] footer mode  [7] batches  [8] index bytes  [9] footer feeds.
+ * cir_debug_scan_batches copies at most max_rows rows and sets *nrows to the
+ * number recorded. */
+#define CIR_SCAN_BATCH_FIELDS 10
+#define CIR_SCAN_PHASE_FIELDS 10
+int cir_debug_scan_timing(cir_ctx* ctx, int enable);
+int cir_debug_scan_batches(cir_ctx* ctx, double* rows, size_t max_rows, size_t* nrows);
+int cir_debug_scan_phases(cir_ctx* ctx, double out[CIR_SCAN_PHASE_FIELDS]);
+
+/* The footer's host BLAKE2b-256 fed in `piece`-byte updates (0 = one
+ * update): no device involved; the CPU tests check it against the oracle. */
+int cir_debug_host_blake2b256(const uint8_t* p, size_t n, size_t piece,
+                              uint8_t out[CIR_DIGEST_BYTES]);
 
 /* How many whole blocks of a file of nfull x block_size bytes (plus any short
  * last block) cir_hash_chunks_dev with a context relays on the calling

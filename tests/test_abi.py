@@ -182,6 +182,35 @@ def test_cli_usage():
     assert p.returncode == 2 and b"usage" in p.stderr
 
 
+def _cli_staging(args, tmp_path):
+    """The staging size the CLI picks for its inputs (printed under
+    CIR_TRACE before cir_init, which then fails: no device here)."""
+    cli = os.path.join(ROOT, "bin", "ciruela-index")
+    env = dict(os.environ, CIR_TRACE="1")
+    p = subprocess.run([cli] + args, capture_output=True, env=env, cwd=str(tmp_path))
+    m = re.search(rb"staging (\d+) bytes per slot", p.stderr)
+    assert m, p.stderr
+    return int(m.group(1))
+
+
+def test_cli_staging_follows_top_level_symlinks(tmp_path):
+    """The one-shot CLI sizes its staging slots from the input's bytes; a
+    symlinked SRC directory or FILE counts its target (the scan and the hash
+    path follow it), a pipe gets the default (0); entries inside a tree are
+    not followed, as the scan does not follow them."""
+    tree = tmp_path / "tree"
+    tree.mkdir()
+    (tree / "a.bin").write_bytes(os.urandom(3 << 20))
+    os.symlink(str(tree), tmp_path / "link")
+    os.symlink(str(tree / "a.bin"), tmp_path / "flink")
+    (tree / "inner").symlink_to(tmp_path / "tree" / "a.bin")  # not followed
+    mib = 1 << 20
+    assert _cli_staging(["sync", "--append", str(tree) + ":/x"], tmp_path) == 3 * mib
+    assert _cli_staging(["sync", "--append", str(tmp_path / "link") + ":/x"], tmp_path) == 3 * mib
+    assert _cli_staging(["hash", str(tmp_path / "flink")], tmp_path) == 3 * mib
+    assert _cli_staging(["hash", "/dev/stdin"], tmp_path) == 0
+
+
 BAD_PATH_INDEXES = [
     # fill_dirs accepts only RootDir / Normal components (src/cluster/download.rs:120-145)
     b"DIRSIGNATURE.v1 blake2b/256 block_size=4096\n/\n/../etc\n  passwd f 0\n",

@@ -1,0 +1,59 @@
+"""The index footer's host BLAKE2b-256 (CPU only, no device involved).
+
+cir_scan_v1 hashes a blake2b/256 index's footer -- ImageId = H(every byte
+after the header line), dir_signature::get_hash read back by
+InMemoryIndexes::register_index (reference src/index.rs:98-105) -- on one host
+thread fed in stretches as the index is emitted (scan.cpp HostFooter,
+blake2b_host.cpp).  It is product code, not the oracle; here it is checked
+against the oracle, the golden vectors and hashlib, over every way a stream
+can be cut: piece sizes around the 128-B block edge, single bytes, and the
+empty input.  The GPU side of the same footer is test_scan_footer_modes in
+tests/test_gpu_parity.py.
+"""
+import ctypes
+import hashlib
+import os
+import random
+
+from conftest import oracle_digest
+from make_golden import gen_bytes
+
+from ciruela_amd import _native
+
+
+def host_digest(data, piece=0):
+    out = ctypes.create_string_buffer(32)
+    buf = ctypes.create_string_buffer(bytes(data), max(1, len(data)))
+    _native.check(_native.lib.cir_debug_host_blake2b256(buf, len(data), piece, out))
+    return out.raw
+
+
+def test_golden_vectors_one_update(vectors):
+    for v in vectors["vectors"]:
+        assert host_digest(gen_bytes(v)).hex() == v["blake2b256"], (v["gen"], v["n"])
+
+
+def test_pieces_across_block_edges(oracle):
+    rng = random.Random(11)
+    for n in [0, 1, 127, 128, 129, 255, 256, 257, 1000, 4096, 65 * 1000 + 3]:
+        data = os.urandom(n)
+        want = oracle_digest(oracle, data)
+        for piece in [0, 1, 63, 127, 128, 129, 256, 1000, rng.randrange(1, 600)]:
+            assert host_digest(data, piece) == want, (n, piece)
+
+
+def test_index_sized_text_against_hashlib():
+    """A 2.3 MiB index-like body (hex digest lines) fed in 256 KiB stretches,
+    the scan's feed size, plus a ragged last stretch."""
+    lines = b"".join(b"  f%05d f 32768 %s\n" % (i, os.urandom(32).hex().encode())
+                     for i in range(30000))
+    assert len(lines) % (256 << 10) != 0
+    assert host_digest(lines, 256 << 10) == hashlib.blake2b(lines, digest_size=32).digest()
+
+
+def test_reference_fixture_rule(dirsig_example):
+    """The footer rule of the reference's fixture (src/cluster/download.rs:
+    357-366) with this hasher: H(body) as the last line, here for blake2b."""
+    idx = dirsig_example["index"].encode()
+    body = idx[idx.index(b"\n") + 1:-65]
+    assert host_digest(body, 7) == hashlib.blake2b(body, digest_size=32).digest()

@@ -702,17 +702,84 @@ def test_desc_quad_mode_edges(gpu, ctx, oracle):
     assert first_bad(out.cpu().numpy(), want) is None
 
 
-def test_scan_long_index_footer(gpu, small_ctx, tmp_path):
-    """An index body of several MiB (128-byte blocks): the footer chain is fed
-    to the device in >= 1 MiB pieces while later batches hash (scan.cpp
-    FooterChain) and must still equal H(body) (src/index.rs:98-105)."""
+@pytest.mark.parametrize("mode", ["host", "gpu"])
+def test_scan_long_index_footer(gpu, small_ctx, tmp_path, mode):
+    """An index body of several MiB (128-byte blocks): the footer is fed in
+    stretches while later batches hash -- to the host thread (scan.cpp
+    HostFooter, the default) or to the device chain in >= 256 KiB pieces
+    (FooterChain) -- and must still equal H(body) (src/index.rs:98-105)."""
     rng = random.Random(5)
     for k in range(6):
         (tmp_path / ("f%d.bin" % k)).write_bytes(rng.randbytes(rng.randrange(1 << 20, 3 << 20)))
     cfg = gpu.ScannerConfig.new().block_size(128).add_dir(str(tmp_path), "/")
-    got = gpu.v1.scan(cfg, context=small_ctx)
+    small_ctx.set_footer_mode(small_ctx.FOOTER_HOST if mode == "host" else small_ctx.FOOTER_GPU)
+    small_ctx.scan_timing(True)
+    try:
+        got = gpu.v1.scan(cfg, context=small_ctx)
+        ph = small_ctx.scan_phases()
+    finally:
+        small_ctx.scan_timing(False)
+        small_ctx.set_footer_mode(small_ctx.FOOTER_HOST)
     assert len(got) > (4 << 20)
     assert got == dirsig_oracle.scan(str(tmp_path), 128)
+    assert ph["footer_mode"] == (0 if mode == "host" else 1)
+    assert ph["footer_feeds"] >= 8 and ph["footer_busy_ms"] > 0
+    assert ph["index_bytes"] == len(got)
+
+
+def test_scan_timing_rows(gpu, tmp_path):
+    """cir_debug_scan_timing: one row per staged batch (bytes add up to the
+    tree's, block counts to its blocks), each batch's events in order (reads,
+    then upload, then hash and digests back), and a phase record per scan."""
+    ctx = gpu.Context(device_mask=1, staging_bytes=4 << 20)
+    rng = random.Random(9)
+    sizes = [rng.randrange(0, 3 << 20) for _ in range(20)]
+    for k, n in enumerate(sizes):
+        (tmp_path / ("f%02d" % k)).write_bytes(rng.randbytes(n))
+    cfg = gpu.ScannerConfig.new().threads(4).add_dir(str(tmp_path), "/")
+    ctx.scan_timing(True)
+    got = gpu.v1.scan(cfg, context=ctx)
+    rows, ph = ctx.scan_batches(), ctx.scan_phases()
+    ctx.scan_timing(False)
+    assert got == dirsig_oracle.scan(str(tmp_path), 32768)
+    assert len(rows) == ph["batches"] >= 10
+    assert sum(r["blocks"] for r in rows) == sum((n + 32767) // 32768 for n in sizes)
+    assert sum(r["bytes"] for r in rows) >= sum(sizes)  # + 16-B alignment of file segments
+    eps = 0.05  # ms: event vs host clock
+    for r in rows:
+        assert r["device"] == 0
+        assert 0 <= r["read_start_ms"] <= r["read_end_ms"] <= r["h2d_start_ms"] + eps
+        assert r["h2d_start_ms"] <= r["h2d_end_ms"] <= r["hash_start_ms"] + eps
+        assert r["hash_start_ms"] <= r["done_ms"]
+    assert ph["hash_loop_ms"] > 0 and ph["footer_mode"] == 0
+    # off: a later scan records nothing
+    gpu.v1.scan(cfg, context=ctx)
+    assert len(ctx.scan_batches()) == len(rows)
+
+
+def test_lazy_staging_context(gpu, oracle):
+    """CIR_STAGING_LAZY: cir_init pins no staging slots (the device-resident
+    line of every rank of a multi-GPU run), the *_dev entry points work at
+    once, and the first host-path call allocates the slots itself."""
+    import torch
+
+    def rss():
+        with open("/proc/self/status") as f:
+            return next(int(ln.split()[1]) << 10 for ln in f if ln.startswith("VmRSS:"))
+    gpu.Context(device_mask=1, staging_bytes=1 << 20).close()  # runtime warm-up
+    r0 = rss()
+    c = gpu.Context(device_mask=1, staging_bytes=gpu._n.CIR_STAGING_LAZY)
+    assert rss() - r0 < (96 << 20), (rss() - r0) >> 20  # an eager context pins 768 MiB
+    data = dev_random(gpu, 1 << 20, 0x1A2)
+    out = torch.empty(32 * 32, dtype=torch.uint8, device="cuda:0")
+    c.hash_chunks_dev(data.data_ptr(), 1 << 20, 32768, out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    host = data.cpu().numpy()
+    assert first_bad(out.cpu().numpy(), oracle_chunks(oracle, host, 1 << 20, 32768)) is None
+    blob = host.tobytes()
+    assert c.hash_memory(blob, 4096) == b"".join(
+        oracle_digest(oracle, blob[i:i + 4096]) for i in range(0, len(blob), 4096))
+    c.close()
 
 
 def test_concurrent_callers_one_context(gpu, small_ctx, oracle):
@@ -837,7 +904,10 @@ def test_multi_device_split_paths(gpu, oracle, tmp_path):
         (d / ("f%02d" % k)).write_bytes(rng.randbytes(rng.choice([0, 1, 5000, 70000, 1 << 20])))
     for block_size in (32768, 1024):
         cfg = gpu.ScannerConfig.new().block_size(block_size).threads(4).add_dir(str(tree), "/")
-        assert gpu.v1.scan(cfg, context=ctx) == dirsig_oracle.scan(str(tree), block_size)
+        want = dirsig_oracle.scan(str(tree), block_size)
+        for mode in (ctx.FOOTER_HOST, ctx.FOOTER_GPU):
+            ctx.set_footer_mode(mode)
+            assert gpu.v1.scan(cfg, context=ctx) == want, (block_size, mode)
 
 
 def test_error_paths_are_codes_not_aborts(gpu, small_ctx, tmp_path):
@@ -1385,9 +1455,10 @@ def test_desc_relay_unordered_lengths_in_one_bin(gpu, ctx, oracle, regime):
 
 
 def test_context_lifecycle_releases_device_memory(gpu, oracle):
-    """cir_init allocates a device state's whole working set up front (three
-    staging slots, ordering and relay scratch, footer-chain buffers) and
-    cir_destroy must give all of it back.  The first two cycles of a process
+    """cir_init allocates a device state's working set up front (three
+    staging slots, ordering and relay scratch, the footer chain's state; the
+    chain's text buffers and timing events on first use) and cir_destroy
+    must give all of it back.  The first two cycles of a process
     leave ~0.2 GiB with the HIP runtime for good (its own lazily created
     state; tools/lifecycle_probe.py: 184 + 24 MiB, then 0 per cycle), so
     after two warm-up cycles ten more create / use / destroy cycles of a

@@ -133,3 +133,50 @@ def test_bench_launches_ranks_itself():
     assert rec["n_gpus"] == 2 and rec["ranks_seen"] == 2
     assert rec["config"]["workload"] == "config4"
     assert sorted(map(tuple, rec["shards"])) == [(0, 64), (64, 64)]
+
+
+def _run_bench(args, timeout=240):
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args,
+                          capture_output=True, text=True, timeout=timeout, env=env)
+
+
+def _line(r):
+    import json
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, (r.stdout, r.stderr[-2000:])
+    return json.loads(lines[0])
+
+
+def test_bad_digest_on_rank1_fails_the_job_line():
+    """Rank 1 corrupts one digest of its shard: the line rank 0 prints says
+    FAIL and names rank 1 (parity is reduced over the job, not rank 0's
+    view), and the job exits non-zero."""
+    r = _run_bench(["--gpus", "2", "--dist-backend", "gloo", "--dry-run", "--steps", "2",
+                    "--blocks", "64", "--dry-run-bad-rank", "1"])
+    rec = _line(r)
+    assert r.returncode != 0
+    assert rec["parity"].startswith("FAIL") and "rank(s) 1" in rec["parity"]
+    assert [p["mismatches"] for p in rec["per_rank"]] == [0, 1]
+    assert rec["parity_checked_blocks"] == sum(p["checked"] for p in rec["per_rank"]) > 0
+    # and clean shards on both ranks pass
+    r = _run_bench(["--gpus", "2", "--dist-backend", "gloo", "--dry-run", "--steps", "2",
+                    "--blocks", "64"])
+    rec = _line(r)
+    assert r.returncode == 0 and rec["parity"] == "ok"
+    assert [p["kernel_ms_avg"] for p in rec["per_rank"]] == [10.0, 11.0]
+
+
+def test_force_dist_launches_one_rank():
+    """`bench.py --gpus 1 --force-dist` with no launcher starts one rank
+    through torch.distributed.run (the N>1 code path at world size 1)."""
+    r = _run_bench(["--gpus", "1", "--force-dist", "--dist-backend", "gloo", "--dry-run",
+                    "--steps", "2", "--blocks", "16"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "launching 1 ranks" in r.stderr
+    rec = _line(r)
+    assert rec["ranks_seen"] == 1 and rec["config"]["workload"] == "config4"
+    assert rec["parity"] == "ok"

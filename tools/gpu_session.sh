@@ -78,6 +78,16 @@ for s in "$@"; do
       step bench 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench.json \
         2> gpurun_out/bench.err
       cat gpurun_out/bench.json ;;
+    forcedist)  # the N>1 code path (process group over RCCL, config 4) on one self-launched rank
+      step forcedist 600 python3 bench.py --gpus 1 --force-dist --steps 20 --warmup 3 \
+        > gpurun_out/forcedist.json 2> gpurun_out/forcedist.err
+      cat gpurun_out/forcedist.json ;;
+    cfg5footer)  # config 5 with the footer on the host thread and on the GPU chain, alternating
+      step cfg5footer 900 python bench.py --workload config5 --footer "${FOOTER:-ab}" \
+        --steps "${STEPS:-3}" --tree-gib "${TREE_GIB:-50}" \
+        > gpurun_out/cfg5footer.json 2> gpurun_out/cfg5footer.err
+      rm -rf /dev/shm/ciruela_bench_tree
+      python3 tools/cfg5_report.py gpurun_out/cfg5footer.json ;;
     cfg2sha)
       step cfg2sha 600 python bench.py --workload config2sha --steps 10 --warmup 2 \
         > gpurun_out/cfg2sha.json 2> gpurun_out/cfg2sha.err
