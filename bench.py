@@ -242,13 +242,15 @@ def timed_steps(step, steps, sync, barrier=None):
 
 
 def max_over_ranks(seconds, device=None):
-    """The slowest rank's time: all_reduce(MAX) over the process group (a
-    no-op at world size 1).  device: where the reduced tensor lives (the
+    """The slowest rank's time: all_reduce(MAX) over the process group (the
+    identity without one).  device: where the reduced tensor lives (the
     rank's GPU for RCCL, None = host memory for gloo)."""
     import torch
     import torch.distributed as dist
     t = torch.tensor([seconds], dtype=torch.float64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    # run whenever a process group exists, world size 1 included, so that a
+    # one-rank --force-dist run exercises the same RCCL call as N ranks
+    if dist.is_available() and dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -281,7 +283,7 @@ def job_summary(rank_stats, device=None):
     import torch
     import torch.distributed as dist
     t = torch.tensor([float(x) for x in rank_stats], dtype=torch.float64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized():  # world size 1 included
         parts = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
         dist.all_gather(parts, t)
     else:
@@ -737,11 +739,14 @@ def run_config5(args, ca, ctx, ctx_init_s=None):
         for d in sample:
             cpu_indexer.index(d, 32768, th, lib)
         return sample_bytes
-    rates = cpu_rates(run, args.cpu_seconds)
-    cpu = cpu_record(rates, "the tree's directories d00..d03 (%d files, %.2f GiB) indexed by "
-                     "oracle/cpu_indexer.py (file-level pool, block_size reads, C BLAKE2b); "
-                     "4 threads = reference default --disk-threads" % (
-                         sum(len(os.listdir(d)) for d in sample), sample_bytes / GIB))
+    if getattr(args, "no_cpu_baseline", False):
+        cpu = {"skipped": "--no-cpu-baseline"}
+    else:
+        rates = cpu_rates(run, args.cpu_seconds)
+        cpu = cpu_record(rates, "the tree's directories d00..d03 (%d files, %.2f GiB) indexed by "
+                         "oracle/cpu_indexer.py (file-level pool, block_size reads, C BLAKE2b); "
+                         "4 threads = reference default --disk-threads" % (
+                             sum(len(os.listdir(d)) for d in sample), sample_bytes / GIB))
     cpu["full_tree"] = {"seconds": round(full_s, 3), "cores": per_gpu_share(),
                         "value": round(nbytes / full_s / GIB, 4)}
     return {"metric": "GiB/s end-to-end index of a tmpfs tree (config 5)",

@@ -123,6 +123,12 @@ unsigned host_copy_threads() {
   return n;
 }
 
+unsigned host_copy_threads(size_t ndev) {
+  if (ndev <= 1) return host_copy_threads();
+  const unsigned share = std::max(host_copy_threads(), usable_cpus() * 3u / 4u);
+  return (unsigned)std::min<size_t>(share, (size_t)kMaxCopyThreads * ndev);
+}
+
 int Device::ensure_slot(Slot& s, uint64_t bytes, uint64_t nblk) {
   if (!s.copied) {
     CIR_HIP(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));

@@ -78,6 +78,10 @@ bool trace_enabled();
 // (profiles/r03_s2/cfg5_threads/): 12 readers 39.1-44.1 GiB/s, 16 readers
 // 32.2-42.1 (the uploads slowed to 6.4-6.7 ms per 256 MiB batch from 5.1-5.9).
 unsigned host_copy_threads();
+// The scan's auto_threads over ndev devices: kMaxCopyThreads readers per
+// device (each device's range is read by threads / ndev of them), within 3/4
+// of the process's CPUs but never fewer than the one-device count.
+unsigned host_copy_threads(size_t ndev);
 
 struct Device {
   int id = 0;

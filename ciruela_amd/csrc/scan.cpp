@@ -13,6 +13,7 @@
 // a directory line, its files and symlinks sorted by name (bytewise), then
 // its subdirectories recursively in name order.
 #include <dirent.h>
+#include <emmintrin.h>
 #include <stdio.h>
 #include <errno.h>
 #include <fcntl.h>
@@ -124,29 +125,72 @@ struct ReadJob {
   uint8_t* dst;
 };
 
+// How the readers move file bytes into a staging slot:
+//   direct (default): pread() straight into the pinned slot -- the kernel's
+//     copy_to_user writes the slot with ordinary stores (read-for-ownership,
+//     the lines left dirty in the CPU caches the upload then snoops);
+//   nt (CIR_SCAN_COPY=nt): pread() into a per-thread 512 KiB bounce buffer
+//     that stays in the core's L2, then non-temporal 16-B stores into the
+//     slot (no read-for-ownership, nothing left in the caches), the way
+//     glibc's memcpy fills the slots of the host-memory paths.
+enum class ReadCopy { kDirect, kNonTemporal };
+static ReadCopy read_copy_mode() {  // read per batch (tests switch it in one process)
+  const char* v = std::getenv("CIR_SCAN_COPY");
+  return v && strcmp(v, "nt") == 0 ? ReadCopy::kNonTemporal : ReadCopy::kDirect;
+}
+
+constexpr size_t kBounce = 512u << 10;
+
+// n bytes from an L2-resident buffer to the slot with streaming stores
+// (16-B aligned destination prefix handled with plain stores).
+static void stream_copy(uint8_t* dst, const uint8_t* src, size_t n) {
+  while (n && (reinterpret_cast<uintptr_t>(dst) & 15u)) {
+    *dst++ = *src++;
+    --n;
+  }
+  size_t i = 0;
+  for (; i + 64 <= n; i += 64) {
+    const __m128i a = _mm_loadu_si128((const __m128i*)(src + i));
+    const __m128i b = _mm_loadu_si128((const __m128i*)(src + i + 16));
+    const __m128i c = _mm_loadu_si128((const __m128i*)(src + i + 32));
+    const __m128i d = _mm_loadu_si128((const __m128i*)(src + i + 48));
+    _mm_stream_si128((__m128i*)(dst + i), a);
+    _mm_stream_si128((__m128i*)(dst + i + 16), b);
+    _mm_stream_si128((__m128i*)(dst + i + 32), c);
+    _mm_stream_si128((__m128i*)(dst + i + 48), d);
+  }
+  memcpy(dst + i, src + i, n - i);
+}
+
 static int run_reads(const std::vector<ReadJob>& jobs, const std::vector<ScanFile>& files,
                      unsigned threads) {
   std::atomic<size_t> next{0};
   std::atomic<int> rc{0};
   std::string err;
   std::mutex err_mu;
+  const bool nt = read_copy_mode() == ReadCopy::kNonTemporal;
   auto worker = [&] {
+    std::unique_ptr<uint8_t[]> bounce(nt ? new uint8_t[kBounce] : nullptr);
     for (;;) {
       const size_t i = next.fetch_add(1);
-      if (i >= jobs.size() || rc.load()) return;
+      if (i >= jobs.size() || rc.load()) break;
       const ReadJob& j = jobs[i];
       const std::string& path = files[j.file].real;
       const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
       bool ok = fd >= 0;
       uint64_t got = 0;
       while (ok && got < j.len) {
-        const ssize_t r = pread(fd, j.dst + got, j.len - got, (off_t)(j.file_off + got));
+        const size_t want = nt ? (size_t)std::min<uint64_t>(kBounce, j.len - got)
+                               : (size_t)(j.len - got);
+        const ssize_t r = pread(fd, nt ? bounce.get() : j.dst + got, want,
+                                (off_t)(j.file_off + got));
         if (r < 0 && errno == EINTR) continue;
         if (r <= 0) {
           ok = false;
           if (r == 0) errno = ENODATA;  // file shrank during the scan
           break;
         }
+        if (nt) stream_copy(j.dst + got, bounce.get(), (size_t)r);
         got += (uint64_t)r;
       }
       const int e = errno;
@@ -155,9 +199,10 @@ static int run_reads(const std::vector<ReadJob>& jobs, const std::vector<ScanFil
         std::lock_guard<std::mutex> lk(err_mu);
         if (!rc.load()) err = "error reading " + path + ": " + strerror(e);
         rc.store(CIR_EIO);
-        return;
+        break;
       }
     }
+    if (nt) _mm_sfence();  // the streamed bytes are globally visible before the upload
   };
   const unsigned n = std::max(1u, std::min<unsigned>(threads, (unsigned)jobs.size()));
   if (n == 1) {
@@ -614,7 +659,7 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
   const bool incremental = hash_type == CIR_HASH_BLAKE2B_256;
   const bool host_footer = incremental && ctx->footer == CIR_FOOTER_HOST;
   const bool gpu_chain = incremental && !host_footer;
-  if (threads == 0) threads = host_copy_threads();  // auto_threads
+  if (threads == 0) threads = host_copy_threads(ctx->devs.size());  // auto_threads
   bool stats;
   size_t rows0;  // this scan's batches are the rows recorded from here on
   {

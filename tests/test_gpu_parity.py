@@ -405,7 +405,12 @@ def make_tree(root):
     os.symlink("target with space", root / "dangling")
 
 
-def test_scan_vs_oracle(gpu, small_ctx, tmp_path):
+@pytest.mark.parametrize("copy", ["direct", "nt"])
+def test_scan_vs_oracle(gpu, small_ctx, tmp_path, copy, monkeypatch):
+    """v1::scan of a tree with every entry kind, at 1, 4 and auto reader
+    threads, with the readers' two copy modes (pread straight into the
+    pinned slot, or through a bounce buffer and streaming stores)."""
+    monkeypatch.setenv("CIR_SCAN_COPY", copy)
     make_tree(tmp_path)
     want = dirsig_oracle.scan(str(tmp_path), 32768)
     for threads in (1, 4, 0):  # 0: auto_threads (the library's host_copy_threads)

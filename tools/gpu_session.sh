@@ -88,10 +88,24 @@ for s in "$@"; do
         > gpurun_out/cfg5footer.json 2> gpurun_out/cfg5footer.err
       rm -rf /dev/shm/ciruela_bench_tree
       python3 tools/cfg5_report.py gpurun_out/cfg5footer.json ;;
+    cfg5copy)  # config 5 with the readers' two copy modes, alternating processes, one tree
+      for rep in $(seq 1 "${REPS:-2}"); do
+        for mode in direct nt; do
+          CIR_SCAN_COPY=$mode step "cfg5copy_$mode" 600 python bench.py --workload config5 \
+            --steps "${STEPS:-3}" --tree-gib "${TREE_GIB:-50}" --no-cpu-baseline \
+            > "gpurun_out/cfg5copy_${mode}_$rep.json" 2> "gpurun_out/cfg5copy_${mode}_$rep.err"
+          echo "== $mode rep $rep"
+          python3 tools/cfg5_report.py "gpurun_out/cfg5copy_${mode}_$rep.json"
+        done
+      done
+      rm -rf /dev/shm/ciruela_bench_tree ;;
     cfg2sha)
       step cfg2sha 600 python bench.py --workload config2sha --steps 10 --warmup 2 \
         > gpurun_out/cfg2sha.json 2> gpurun_out/cfg2sha.err
       cat gpurun_out/cfg2sha.json ;;
+    crossover)  # cir_verify_blocks batch vs the drop-in vs one host core, 32 KiB blocks
+      step crossover 300 python tools/verify_crossover.py > gpurun_out/crossover.log 2>&1
+      cat gpurun_out/crossover.log ;;
     latency)
       step latency 300 python tools/hash_bytes_latency.py > gpurun_out/latency.log 2>&1
       cat gpurun_out/latency.log ;;
