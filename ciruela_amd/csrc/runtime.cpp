@@ -332,8 +332,9 @@ static int slot_submit_impl(Device& d, Slot& s, uint64_t bytes, uint64_t nblk,
   } else
     CIR_HIP(dev::launch_chunks(src, bytes, chunk_bs, s.d_out, d.compute));
   CIR_HIP(hipMemcpyAsync(s.h_out, s.d_out, nblk * 32, hipMemcpyDeviceToHost, d.compute));
-  CIR_HIP(hipEventRecord(s.done, d.compute));
+  // t_done before done: slot_wait's synchronize on done then covers it
   if (s.timed) CIR_HIP(hipEventRecord(s.t_done, d.compute));
+  CIR_HIP(hipEventRecord(s.done, d.compute));
   s.busy = true;
   return CIR_OK;
 }

@@ -289,3 +289,21 @@ def test_descriptor_count_limit():
         rc = lib.cir_hash_blocks_dev_ht(None, _native.CIR_HASH_BLAKE2B_256, 16, 16, 16, n, 32, None)
         assert rc == _native.CIR_EINVAL
         assert b"2^31-1" in lib.cir_last_error()
+
+
+def test_product_never_loads_the_oracle():
+    """The oracle is test infrastructure: the library exports and imports
+    nothing of it, and no product source names its library or modules (the
+    footer's host BLAKE2b is the product's own, blake2b_host.cpp)."""
+    out = subprocess.check_output(["nm", "-D", _native.LIB_PATH]).decode()
+    assert "oracle_" not in out
+    libs = subprocess.check_output(["readelf", "-d", _native.LIB_PATH]).decode()
+    assert "oracle" not in libs
+    srcs = glob.glob(os.path.join(ROOT, "ciruela_amd", "**", "*.*"), recursive=True)
+    for p in srcs:
+        if not p.endswith((".py", ".cpp", ".hpp", ".hip", ".h")):
+            continue
+        text = open(p, errors="replace").read()
+        for bad in ("liboracle", "blake2b_oracle", "import cpu_indexer", "import dirsig_oracle",
+                    "oracle/"):
+            assert bad not in text, (p, bad)
