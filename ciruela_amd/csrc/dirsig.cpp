@@ -5,6 +5,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+
 namespace cir {
 namespace dirsig {
 
@@ -91,43 +93,83 @@ bool from_hex(const std::string& s, std::vector<uint8_t>* out) {
 Emitter::Emitter(const Header& h) {
   header_ = std::string("DIRSIGNATURE.v1 ") + hash_type_name(h.hash) +
             " block_size=" + std::to_string(h.block_size) + "\n";
+  append(header_);
+  hlen_ = len_;
+}
+
+Emitter::~Emitter() { free(buf_); }
+
+bool Emitter::reserve_body(size_t n) {
+  if (len_ + n <= cap_) return true;
+  uint8_t* p = (uint8_t*)realloc(buf_, len_ + n);
+  if (!p) return false;
+  buf_ = p;
+  cap_ = len_ + n;
+  return true;
+}
+
+char* Emitter::grow(size_t n) {
+  if (oom_) return nullptr;
+  if (len_ + n > cap_) {
+    // doubling; realloc of a large block remaps its pages instead of copying
+    const size_t cap = std::max(len_ + n, std::max<size_t>(cap_ * 2, 4096));
+    uint8_t* p = (uint8_t*)realloc(buf_, cap);
+    if (!p) {
+      oom_ = true;
+      return nullptr;
+    }
+    buf_ = p;
+    cap_ = cap;
+  }
+  char* at = (char*)buf_ + len_;
+  len_ += n;
+  return at;
+}
+
+void Emitter::append(const char* p, size_t n) {
+  if (char* at = grow(n)) memcpy(at, p, n);
 }
 
 void Emitter::start_dir(const std::string& vpath) {
-  body_ += escape(vpath);
-  body_ += '\n';
+  append(escape(vpath));
+  append("\n", 1);
 }
 
 void Emitter::add_file(const std::string& name, bool exe, uint64_t size, const uint8_t* hashes,
                        size_t nhash) {
-  body_ += "  ";
-  body_ += escape(name);
-  body_ += exe ? " x " : " f ";
-  body_ += std::to_string(size);
+  append("  ", 2);
+  append(escape(name));
+  append(exe ? " x " : " f ", 3);
+  append(std::to_string(size));
+  // " " + 64 hex digits per digest, written in place
+  char* at = grow(65 * nhash + 1);
+  if (!at) return;
   for (size_t i = 0; i < nhash; ++i) {
-    body_ += ' ';
-    body_ += to_hex(hashes + 32 * i, 32);
+    *at++ = ' ';
+    const uint8_t* h = hashes + 32 * i;
+    for (int k = 0; k < 32; ++k) {
+      *at++ = kHex[h[k] >> 4];
+      *at++ = kHex[h[k] & 15];
+    }
   }
-  body_ += '\n';
+  *at = '\n';
 }
 
 void Emitter::add_symlink(const std::string& name, const std::string& target) {
-  body_ += "  ";
-  body_ += escape(name);
-  body_ += " s ";
-  body_ += escape(target);
-  body_ += '\n';
+  append("  ", 2);
+  append(escape(name));
+  append(" s ", 3);
+  append(escape(target));
+  append("\n", 1);
 }
 
-uint8_t* Emitter::finish_malloc(const uint8_t* footer, size_t footer_len, size_t* len) const {
-  const std::string tail = to_hex(footer, footer_len) + '\n';
-  const size_t n = header_.size() + body_.size() + tail.size();
-  uint8_t* out = (uint8_t*)malloc(n);
-  if (!out) return nullptr;
-  memcpy(out, header_.data(), header_.size());
-  memcpy(out + header_.size(), body_.data(), body_.size());
-  memcpy(out + header_.size() + body_.size(), tail.data(), tail.size());
-  *len = n;
+uint8_t* Emitter::finish_malloc(const uint8_t* footer, size_t footer_len, size_t* len) {
+  append(to_hex(footer, footer_len) + '\n');
+  if (oom_) return nullptr;
+  uint8_t* out = buf_;
+  *len = len_;
+  buf_ = nullptr;
+  len_ = cap_ = hlen_ = 0;
   return out;
 }
 

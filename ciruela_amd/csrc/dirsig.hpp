@@ -39,24 +39,40 @@ struct Header {
 };
 
 // Streaming emitter: header, then for each directory start_dir + entries;
-// finish_malloc() needs the footer digest of body() (computed by the caller on
-// the GPU) and appends its hex line.
+// finish_malloc() needs the footer digest of the body (computed by the
+// caller) and appends its hex line.  The index is built in place in one
+// malloc'd buffer (header first), so finishing hands that buffer over
+// without copying the body.
 class Emitter {
  public:
   explicit Emitter(const Header& h);
+  ~Emitter();
+  Emitter(const Emitter&) = delete;
+  Emitter& operator=(const Emitter&) = delete;
+  // room for n more body bytes (an estimate: appends still grow the buffer)
+  bool reserve_body(size_t n);
   void start_dir(const std::string& vpath);  // "/" or "/a/b" (raw bytes)
   void add_file(const std::string& name, bool exe, uint64_t size, const uint8_t* hashes,
                 size_t nhash);
   void add_symlink(const std::string& name, const std::string& target);
-  // Bytes the footer hashes: everything after the header line.
-  const std::string& body() const { return body_; }
-  // header + body + hex footer + newline in one malloc'd buffer (free()); null if out of memory
-  uint8_t* finish_malloc(const uint8_t* footer, size_t footer_len, size_t* len) const;
+  // Bytes the footer hashes: everything after the header line.  The pointer
+  // moves when the buffer grows; an offset into the body stays valid.
+  const char* body_data() const { return (const char*)buf_ + hlen_; }
+  size_t body_size() const { return len_ - hlen_; }
+  // header + body + hex footer + newline in one malloc'd buffer (free()),
+  // which the emitter gives up; null if out of memory (or after an append
+  // failed to allocate).
+  uint8_t* finish_malloc(const uint8_t* footer, size_t footer_len, size_t* len);
   const std::string& header_line() const { return header_; }
 
  private:
+  char* grow(size_t n);  // n more bytes at the end; null on allocation failure
+  void append(const char* p, size_t n);
+  void append(const std::string& s) { append(s.data(), s.size()); }
   std::string header_;
-  std::string body_;
+  uint8_t* buf_ = nullptr;
+  size_t len_ = 0, cap_ = 0, hlen_ = 0;
+  bool oom_ = false;
 };
 
 enum class EntryKind { kDir, kFile, kLink };

@@ -4,6 +4,7 @@
 // each entry point replaces.
 #include "runtime.hpp"
 
+#include <emmintrin.h>
 #include <errno.h>
 #include <sched.h>
 #include <stdio.h>
@@ -127,6 +128,84 @@ unsigned host_copy_threads(size_t ndev) {
   if (ndev <= 1) return host_copy_threads();
   const unsigned share = std::max(host_copy_threads(), usable_cpus() * 3u / 4u);
   return (unsigned)std::min<size_t>(share, (size_t)kMaxCopyThreads * ndev);
+}
+
+bool stage_copy_nt() {  // read per call: tests switch it within one process
+  const char* v = std::getenv("CIR_STAGE_COPY");
+  return !(v && strcmp(v, "direct") == 0);
+}
+
+// 16-B aligned non-temporal stores; the unaligned head and the tail with
+// plain stores; sfence so the bytes are globally visible before the caller
+// hands the slot to the copy engine.
+static void stream_copy(uint8_t* dst, const uint8_t* src, size_t n) {
+  while (n && (reinterpret_cast<uintptr_t>(dst) & 15u)) {
+    *dst++ = *src++;
+    --n;
+  }
+  size_t i = 0;
+  for (; i + 64 <= n; i += 64) {
+    const __m128i a = _mm_loadu_si128((const __m128i*)(src + i));
+    const __m128i b = _mm_loadu_si128((const __m128i*)(src + i + 16));
+    const __m128i c = _mm_loadu_si128((const __m128i*)(src + i + 32));
+    const __m128i e = _mm_loadu_si128((const __m128i*)(src + i + 48));
+    _mm_stream_si128((__m128i*)(dst + i), a);
+    _mm_stream_si128((__m128i*)(dst + i + 16), b);
+    _mm_stream_si128((__m128i*)(dst + i + 32), c);
+    _mm_stream_si128((__m128i*)(dst + i + 48), e);
+  }
+  memcpy(dst + i, src + i, n - i);
+  _mm_sfence();
+}
+
+void copy_staged(uint8_t* dst, const uint8_t* src, size_t n) {
+  if (stage_copy_nt() && n >= 4096)
+    stream_copy(dst, src, n);
+  else
+    memcpy(dst, src, n);
+}
+
+// Bounce buffers for pread_staged, reused across calls and threads (the
+// reader threads are created per batch).
+constexpr size_t kBounce = 512u << 10;
+static struct BouncePool {
+  std::mutex mu;
+  std::vector<uint8_t*> free;
+  ~BouncePool() {
+    for (uint8_t* p : free) delete[] p;
+  }
+} g_bounce;
+
+ssize_t pread_staged(int fd, uint8_t* dst, size_t n, off_t off) {
+  if (!stage_copy_nt() || n < 4096) return ::pread(fd, dst, n, off);
+  uint8_t* b = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_bounce.mu);
+    if (!g_bounce.free.empty()) {
+      b = g_bounce.free.back();
+      g_bounce.free.pop_back();
+    }
+  }
+  if (!b) b = new uint8_t[kBounce];
+  size_t got = 0;
+  ssize_t last = 0;
+  while (got < n) {
+    const size_t want = std::min(kBounce, n - got);
+    last = ::pread(fd, b, want, off + (off_t)got);
+    if (last < 0 && errno == EINTR) continue;
+    if (last <= 0) break;
+    stream_copy(dst + got, b, (size_t)last);
+    got += (size_t)last;
+    if ((size_t)last < want) break;  // a short read (EOF): the caller decides
+  }
+  const int e = errno;
+  {
+    std::lock_guard<std::mutex> lk(g_bounce.mu);
+    g_bounce.free.push_back(b);
+  }
+  errno = e;
+  if (got > 0) return (ssize_t)got;
+  return last;  // 0 at EOF, -1 with errno
 }
 
 int Device::ensure_slot(Slot& s, uint64_t bytes, uint64_t nblk) {
@@ -454,7 +533,7 @@ static int run_blocks(cir_ctx* ctx, Device& d, const uint8_t* arena, const uint6
       const size_t base = next;
       parallel_items(n, pos, [&](size_t i0, size_t i1) {
         for (size_t i = i0; i < i1; ++i)
-          memcpy(s.h_data + s.h_off[i], arena + off[base + i], s.h_len[i]);
+          copy_staged(s.h_data + s.h_off[i], arena + off[base + i], s.h_len[i]);
       });
       rc = slot_submit(d, s, std::max<uint64_t>(pos, 1), n, ht);
       if (rc) return rc;
@@ -971,7 +1050,8 @@ int cir_hash_file_ht(cir_ctx* ctx, int hash_type, int fd, uint64_t block_size,
       const int64_t e = parallel_pieces(n, [&](uint64_t o, uint64_t len) -> int64_t {
         uint64_t got = 0;
         while (got < len) {
-          const ssize_t r = ::pread(fd, dst + o + got, len - got, pos0 + (off_t)(off + o + got));
+          const ssize_t r = pread_staged(fd, dst + o + got, len - got,
+                                         pos0 + (off_t)(off + o + got));
           if (r < 0 && errno == EINTR) continue;
           if (r <= 0) return r < 0 ? -(int64_t)errno : (int64_t)got;
           got += (uint64_t)r;
@@ -1001,7 +1081,8 @@ int cir_hash_file_ht(cir_ctx* ctx, int hash_type, int fd, uint64_t block_size,
       const int64_t e = parallel_pieces(k, [&](uint64_t off, uint64_t len) -> int64_t {
         uint64_t got = 0;
         while (got < len) {
-          const ssize_t r = ::pread(fd, dst + off + got, len - got, (off_t)(base + off + got));
+          const ssize_t r = pread_staged(fd, dst + off + got, len - got,
+                                         (off_t)(base + off + got));
           if (r < 0 && errno == EINTR) continue;
           if (r < 0) return -(int64_t)errno;
           if (r == 0) break;  // truncated meanwhile
@@ -1045,7 +1126,7 @@ int cir_hash_memory_ht(cir_ctx* ctx, int hash_type, const uint8_t* data, uint64_
   if (ctx->devs.size() > 1 && size > block_size) {
     PosReader prd = [data](uint8_t* dst, uint64_t n, uint64_t off) -> int64_t {
       parallel_pieces(n, [&](uint64_t o, uint64_t len) -> int64_t {
-        memcpy(dst + o, data + off + o, len);
+        copy_staged(dst + o, data + off + o, len);
         return (int64_t)len;
       });
       return (int64_t)n;
@@ -1060,7 +1141,7 @@ int cir_hash_memory_ht(cir_ctx* ctx, int hash_type, const uint8_t* data, uint64_
     const uint64_t k = std::min(n, size - pos);
     const uint8_t* src = data + pos;
     parallel_pieces(k, [&](uint64_t off, uint64_t len) -> int64_t {
-      memcpy(dst + off, src + off, len);
+      copy_staged(dst + off, src + off, len);
       return (int64_t)len;
     });
     pos += k;

@@ -4,6 +4,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <sys/types.h>
 
 #include <array>
 #include <functional>
@@ -82,6 +83,23 @@ unsigned host_copy_threads();
 // device (each device's range is read by threads / ndev of them), within 3/4
 // of the process's CPUs but never fewer than the one-device count.
 unsigned host_copy_threads(size_t ndev);
+
+// How host threads fill the pinned staging slots (CIR_STAGE_COPY):
+//   nt (the default): non-temporal 16-B stores -- file bytes are pread()
+//     into a per-thread 512 KiB bounce buffer that stays in the core's L2
+//     and streamed from there -- so a slot is written without
+//     read-for-ownership and leaves no dirty lines in the CPU caches for the
+//     upload's DMA reads to meet;
+//   direct: pread() / memcpy() straight into the slot.
+// Config 5 (50 GiB tmpfs tree, one box, alternating processes,
+// profiles/r04/cfg5_copy/): direct 43.8-45.4 GiB/s with every 256 MiB
+// upload at 4.8-6.2 ms while the readers run; nt 47.8-48.6 GiB/s, every
+// upload 4.75 ms (the link's rate) and the reads faster too.
+bool stage_copy_nt();
+// n bytes into a staging slot from memory / from fd at off (pread
+// semantics: the count read, 0 at EOF, -1 with errno), in the stage mode.
+void copy_staged(uint8_t* dst, const uint8_t* src, size_t n);
+ssize_t pread_staged(int fd, uint8_t* dst, size_t n, off_t off);
 
 struct Device {
   int id = 0;

@@ -13,7 +13,6 @@
 // a directory line, its files and symlinks sorted by name (bytewise), then
 // its subdirectories recursively in name order.
 #include <dirent.h>
-#include <emmintrin.h>
 #include <stdio.h>
 #include <errno.h>
 #include <fcntl.h>
@@ -125,72 +124,31 @@ struct ReadJob {
   uint8_t* dst;
 };
 
-// How the readers move file bytes into a staging slot:
-//   direct (default): pread() straight into the pinned slot -- the kernel's
-//     copy_to_user writes the slot with ordinary stores (read-for-ownership,
-//     the lines left dirty in the CPU caches the upload then snoops);
-//   nt (CIR_SCAN_COPY=nt): pread() into a per-thread 512 KiB bounce buffer
-//     that stays in the core's L2, then non-temporal 16-B stores into the
-//     slot (no read-for-ownership, nothing left in the caches), the way
-//     glibc's memcpy fills the slots of the host-memory paths.
-enum class ReadCopy { kDirect, kNonTemporal };
-static ReadCopy read_copy_mode() {  // read per batch (tests switch it in one process)
-  const char* v = std::getenv("CIR_SCAN_COPY");
-  return v && strcmp(v, "nt") == 0 ? ReadCopy::kNonTemporal : ReadCopy::kDirect;
-}
-
-constexpr size_t kBounce = 512u << 10;
-
-// n bytes from an L2-resident buffer to the slot with streaming stores
-// (16-B aligned destination prefix handled with plain stores).
-static void stream_copy(uint8_t* dst, const uint8_t* src, size_t n) {
-  while (n && (reinterpret_cast<uintptr_t>(dst) & 15u)) {
-    *dst++ = *src++;
-    --n;
-  }
-  size_t i = 0;
-  for (; i + 64 <= n; i += 64) {
-    const __m128i a = _mm_loadu_si128((const __m128i*)(src + i));
-    const __m128i b = _mm_loadu_si128((const __m128i*)(src + i + 16));
-    const __m128i c = _mm_loadu_si128((const __m128i*)(src + i + 32));
-    const __m128i d = _mm_loadu_si128((const __m128i*)(src + i + 48));
-    _mm_stream_si128((__m128i*)(dst + i), a);
-    _mm_stream_si128((__m128i*)(dst + i + 16), b);
-    _mm_stream_si128((__m128i*)(dst + i + 32), c);
-    _mm_stream_si128((__m128i*)(dst + i + 48), d);
-  }
-  memcpy(dst + i, src + i, n - i);
-}
-
 static int run_reads(const std::vector<ReadJob>& jobs, const std::vector<ScanFile>& files,
                      unsigned threads) {
   std::atomic<size_t> next{0};
   std::atomic<int> rc{0};
   std::string err;
   std::mutex err_mu;
-  const bool nt = read_copy_mode() == ReadCopy::kNonTemporal;
   auto worker = [&] {
-    std::unique_ptr<uint8_t[]> bounce(nt ? new uint8_t[kBounce] : nullptr);
     for (;;) {
       const size_t i = next.fetch_add(1);
-      if (i >= jobs.size() || rc.load()) break;
+      if (i >= jobs.size() || rc.load()) return;
       const ReadJob& j = jobs[i];
       const std::string& path = files[j.file].real;
       const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
       bool ok = fd >= 0;
       uint64_t got = 0;
       while (ok && got < j.len) {
-        const size_t want = nt ? (size_t)std::min<uint64_t>(kBounce, j.len - got)
-                               : (size_t)(j.len - got);
-        const ssize_t r = pread(fd, nt ? bounce.get() : j.dst + got, want,
-                                (off_t)(j.file_off + got));
+        // into the pinned slot (streaming stores through a bounce buffer by
+        // default: runtime.cpp pread_staged)
+        const ssize_t r = pread_staged(fd, j.dst + got, j.len - got, (off_t)(j.file_off + got));
         if (r < 0 && errno == EINTR) continue;
         if (r <= 0) {
           ok = false;
           if (r == 0) errno = ENODATA;  // file shrank during the scan
           break;
         }
-        if (nt) stream_copy(j.dst + got, bounce.get(), (size_t)r);
         got += (uint64_t)r;
       }
       const int e = errno;
@@ -199,10 +157,9 @@ static int run_reads(const std::vector<ReadJob>& jobs, const std::vector<ScanFil
         std::lock_guard<std::mutex> lk(err_mu);
         if (!rc.load()) err = "error reading " + path + ": " + strerror(e);
         rc.store(CIR_EIO);
-        break;
+        return;
       }
     }
-    if (nt) _mm_sfence();  // the streamed bytes are globally visible before the upload
   };
   const unsigned n = std::max(1u, std::min<unsigned>(threads, (unsigned)jobs.size()));
   if (n == 1) {
@@ -215,6 +172,12 @@ static int run_reads(const std::vector<ReadJob>& jobs, const std::vector<ScanFil
   if (rc.load()) return fail(rc.load(), err);
   return CIR_OK;
 }
+
+// The scan's digests, 32 bytes per block in the global block order.
+struct DigestBuf {
+  std::unique_ptr<uint8_t[]> p;
+  uint8_t* data() { return p.get(); }
+};
 
 // Hash every block of every file; digests[32*g] for global block g.
 // Batches are packed into the two staging slots of device 0 (file segments
@@ -231,7 +194,7 @@ using Progress = std::function<int(uint64_t done_blk)>;
 // since scan_t0 on the host clock; the device's copy stream gets a reference
 // event at the start that maps its HIP event times onto that clock.
 static int hash_range(cir_ctx* ctx, Device& d, size_t di, const std::vector<ScanFile>& files,
-                      uint64_t bs, unsigned threads, int ht, std::vector<uint8_t>& digests,
+                      uint64_t bs, unsigned threads, int ht, DigestBuf& digests,
                       uint64_t b0, uint64_t b1, const std::function<int(uint64_t)>& done,
                       double scan_t0) {
   std::lock_guard<std::mutex> lk(d.mu);
@@ -371,14 +334,17 @@ static int hash_range(cir_ctx* ctx, Device& d, size_t di, const std::vector<Scan
 // global order that is complete, called under a lock on device 0's
 // current-device setting (the emitter feeds device 0's footer chain).
 static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, unsigned threads,
-                      int ht, std::vector<uint8_t>& digests, const Progress& progress,
+                      int ht, DigestBuf& digests, const Progress& progress,
                       double scan_t0) {
   uint64_t nblk_total = 0;
   for (ScanFile& f : files) {
     f.first_blk = nblk_total;
     nblk_total += (f.size + bs - 1) / bs;
   }
-  digests.assign(32 * nblk_total, 0);
+  // not zero-filled: every digest is written before its file is emitted,
+  // and the pages are touched by those copies as the batches come back
+  // instead of up front (52 MB for config 5: ~5-8 ms before the first read)
+  digests.p.reset(new uint8_t[32 * nblk_total]);
   if (nblk_total == 0) return CIR_OK;
   const size_t nd = std::min<size_t>(ctx->devs.size(), nblk_total);
   if (nd <= 1)
@@ -467,7 +433,7 @@ struct FooterChain {
   }
 
   // feed body[fed, fed + n) (n whole lines unless final)
-  int push(const std::string& body, size_t n, bool final) {
+  int push(const dirsig::Emitter& em, size_t n, bool final) {
     while (n > 0 || final) {
       const size_t piece = std::min<size_t>(n, final ? n : (size_t)256 << 20);
       const bool last = final && piece == n;
@@ -488,7 +454,7 @@ struct FooterChain {
                   cap / 1048576.0, now_ms() - ta);
       }
       if (piece) {
-        memcpy(d.chain_h[k], body.data() + fed, piece);
+        memcpy(d.chain_h[k], em.body_data() + fed, piece);
         CIR_HIP(hipMemcpyAsync(d.chain_d[k], d.chain_h[k], piece, hipMemcpyHostToDevice, d.chain));
       }
       hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -512,15 +478,15 @@ struct FooterChain {
   }
 
   // feed what is complete, keeping >= 1 byte back; skip tiny feeds
-  int advance(const std::string& body, size_t min_feed) {
-    const size_t avail = body.size() - fed;
+  int advance(const dirsig::Emitter& em, size_t min_feed) {
+    const size_t avail = em.body_size() - fed;
     const size_t n = avail > 0 ? (avail - 1) / 128 * 128 : 0;
     if (n < min_feed) return CIR_OK;
-    return push(body, n, false);
+    return push(em, n, false);
   }
 
-  int finish(const std::string& body, uint8_t out[32]) {
-    int rc = push(body, body.size() - fed, true);
+  int finish(const dirsig::Emitter& em, uint8_t out[32]) {
+    int rc = push(em, em.body_size() - fed, true);
     if (rc) return rc;
     CIR_HIP(hipMemcpyAsync(out, d.chain_state, 32, hipMemcpyDeviceToHost, d.chain));
     CIR_HIP(hipStreamSynchronize(d.chain));
@@ -542,20 +508,20 @@ class HostFooter {
   size_t feeds() const { return feeds_; }
   double busy_ms() const { return busy_ms_; }  // valid after finish()
 
-  void advance(const std::string& body, size_t min_feed) {
-    const size_t n = body.size() - fed_;
+  void advance(const dirsig::Emitter& em, size_t min_feed) {
+    const size_t n = em.body_size() - fed_;
     if (n == 0 || n < min_feed) return;
     {
       std::lock_guard<std::mutex> lk(mu_);
-      q_.emplace_back(body, fed_, n);
+      q_.emplace_back(em.body_data() + fed_, n);
     }
     cv_.notify_one();
     fed_ += n;
     ++feeds_;
   }
 
-  void finish(const std::string& body, uint8_t out[32]) {
-    advance(body, 0);
+  void finish(const dirsig::Emitter& em, uint8_t out[32]) {
+    advance(em, 0);
     close();
     st_.final(out);
   }
@@ -679,6 +645,17 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
     if (rc) return rc;
   }
   dirsig::Emitter em(hdr);
+  {
+    // the body's size, near enough to grow the buffer once: 65 bytes per
+    // digest plus each line's name and size (escaping may add a little)
+    size_t est = 4096;
+    for (const PlanItem& it : plan) {
+      est += it.name.size() + it.target.size() + 32;
+      if (it.kind == dirsig::EntryKind::kFile)
+        est += 65 * ((files[it.file].size + block_size - 1) / block_size);
+    }
+    if (!em.reserve_body(est + est / 64)) return fail(CIR_ENOMEM, "index buffer");
+  }
   Device& dv = *ctx->devs[0];
   std::unique_lock<std::mutex> chain_lock(dv.chain_mu, std::defer_lock);
   if (gpu_chain) chain_lock.lock();
@@ -689,7 +666,7 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
   if (host_footer) hfoot = std::make_unique<HostFooter>();
   int rc = gpu_chain ? chain.start() : CIR_OK;
   if (rc) return rc;
-  std::vector<uint8_t> digests;
+  DigestBuf digests;
   size_t plan_pos = 0;
   // emit every plan item whose file blocks are all hashed (files complete in
   // plan order), then feed the finished stretch of the body to the footer
@@ -707,8 +684,8 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
         em.add_file(it.name, it.exe, f.size, digests.data() + 32 * f.first_blk, nb);
       }
     }
-    if (hfoot) hfoot->advance(em.body(), (size_t)256 << 10);
-    return gpu_chain ? chain.advance(em.body(), (size_t)256 << 10) : (int)CIR_OK;
+    if (hfoot) hfoot->advance(em, (size_t)256 << 10);
+    return gpu_chain ? chain.advance(em, (size_t)256 << 10) : (int)CIR_OK;
   };
   const double t1 = now_ms();
   rc = hash_files(ctx, files, block_size, threads, hash_type, digests, emit_ready,
@@ -719,18 +696,20 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
   if (rc) return rc;
   const double t3 = now_ms();
   // Footer = H(every byte after the header line).
-  const std::string& body = em.body();
   uint8_t footer[32];
   if (hfoot) {
-    hfoot->finish(body, footer);
+    hfoot->finish(em, footer);
   } else if (gpu_chain) {
-    if (body.size() - chain.fed > 0xffffffffull) return fail(CIR_EINVAL, "index tail above 4 GiB");
-    rc = chain.finish(body, footer);
+    if (em.body_size() - chain.fed > 0xffffffffull)
+      return fail(CIR_EINVAL, "index tail above 4 GiB");
+    rc = chain.finish(em, footer);
   } else {
-    if (body.size() > 0xffffffffull) return fail(CIR_EINVAL, "index body longer than 4 GiB");
+    if (em.body_size() > 0xffffffffull) return fail(CIR_EINVAL, "index body longer than 4 GiB");
     const uint64_t off = 0;
-    const uint32_t blen = (uint32_t)body.size();
-    rc = cir_hash_blocks_ht(ctx, hash_type, (const uint8_t*)body.data(), &off, &blen, 1, footer);
+    const uint32_t blen = (uint32_t)em.body_size();
+    static const uint8_t empty = 0;
+    rc = cir_hash_blocks_ht(ctx, hash_type,
+                            blen ? (const uint8_t*)em.body_data() : &empty, &off, &blen, 1, footer);
   }
   if (rc) return rc;
   const double t4 = now_ms();
@@ -801,15 +780,14 @@ int cir_index_rewrite(cir_ctx* ctx, const uint8_t* in, size_t len, uint8_t** out
   if (!ctx) return fail(CIR_EINVAL, "null ctx");
   dirsig::Emitter em(idx.header);
   emit_tree(em, "/", root);
-  const std::string& body = em.body();
-  if (body.size() > 0xffffffffull) return fail(CIR_EINVAL, "index body longer than 4 GiB");
+  if (em.body_size() > 0xffffffffull) return fail(CIR_EINVAL, "index body longer than 4 GiB");
   uint8_t footer[32];
   const uint64_t off = 0;
-  const uint32_t blen = (uint32_t)body.size();
+  const uint32_t blen = (uint32_t)em.body_size();
   static const uint8_t empty = 0;
   const int ht = idx.header.hash == dirsig::HashType::kSha512_256 ? CIR_HASH_SHA512_256
                                                                    : CIR_HASH_BLAKE2B_256;
-  int rc = cir_hash_blocks_ht(ctx, ht, body.empty() ? &empty : (const uint8_t*)body.data(), &off,
+  int rc = cir_hash_blocks_ht(ctx, ht, blen ? (const uint8_t*)em.body_data() : &empty, &off,
                               &blen, 1, footer);
   if (rc) return rc;
   *out = em.finish_malloc(footer, 32, out_len);

@@ -351,7 +351,9 @@ def test_desc_quad_capacity_overflow(gpu, ctx, oracle):
     assert first_bad(out.cpu().numpy(), want) is None
 
 
-def test_host_blocks_many_batches(small_ctx, oracle):
+@pytest.mark.parametrize("copy", ["direct", "nt"])
+def test_host_blocks_many_batches(small_ctx, oracle, copy, monkeypatch):
+    monkeypatch.setenv("CIR_STAGE_COPY", copy)  # the gather into the slots, both modes
     rng = random.Random(11)
     arena = os.urandom(6 << 20)
     n = 3000
@@ -410,7 +412,7 @@ def test_scan_vs_oracle(gpu, small_ctx, tmp_path, copy, monkeypatch):
     """v1::scan of a tree with every entry kind, at 1, 4 and auto reader
     threads, with the readers' two copy modes (pread straight into the
     pinned slot, or through a bounce buffer and streaming stores)."""
-    monkeypatch.setenv("CIR_SCAN_COPY", copy)
+    monkeypatch.setenv("CIR_STAGE_COPY", copy)
     make_tree(tmp_path)
     want = dirsig_oracle.scan(str(tmp_path), 32768)
     for threads in (1, 4, 0):  # 0: auto_threads (the library's host_copy_threads)
@@ -728,7 +730,7 @@ def test_scan_long_index_footer(gpu, small_ctx, tmp_path, mode):
     assert len(got) > (4 << 20)
     assert got == dirsig_oracle.scan(str(tmp_path), 128)
     assert ph["footer_mode"] == (0 if mode == "host" else 1)
-    assert ph["footer_feeds"] >= 8 and ph["footer_busy_ms"] > 0
+    assert ph["footer_feeds"] >= 3 and ph["footer_busy_ms"] > 0  # fed while the scan ran
     assert ph["index_bytes"] == len(got)
 
 
@@ -838,10 +840,13 @@ def test_concurrent_callers_one_context(gpu, small_ctx, oracle):
     assert errors == []
 
 
-def test_hash_file_parallel_reads_offset_and_pipe(ctx, oracle, tmp_path):
+@pytest.mark.parametrize("copy", ["direct", "nt"])
+def test_hash_file_parallel_reads_offset_and_pipe(ctx, oracle, tmp_path, copy, monkeypatch):
     """Regular files are read with pread by several threads per staging batch
     starting at the fd's current offset, which ends at EOF (the reference
-    reads the Read object to its end); pipes go through plain read()."""
+    reads the Read object to its end); pipes go through plain read().  Both
+    staging copy modes (CIR_STAGE_COPY)."""
+    monkeypatch.setenv("CIR_STAGE_COPY", copy)
     import threading
     bs = 32768
     data = os.urandom((21 << 20) + 5)

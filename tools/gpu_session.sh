@@ -91,7 +91,7 @@ for s in "$@"; do
     cfg5copy)  # config 5 with the readers' two copy modes, alternating processes, one tree
       for rep in $(seq 1 "${REPS:-2}"); do
         for mode in direct nt; do
-          CIR_SCAN_COPY=$mode step "cfg5copy_$mode" 600 python bench.py --workload config5 \
+          CIR_STAGE_COPY=$mode step "cfg5copy_$mode" 600 python bench.py --workload config5 \
             --steps "${STEPS:-3}" --tree-gib "${TREE_GIB:-50}" --no-cpu-baseline \
             > "gpurun_out/cfg5copy_${mode}_$rep.json" 2> "gpurun_out/cfg5copy_${mode}_$rep.err"
           echo "== $mode rep $rep"
@@ -99,6 +99,15 @@ for s in "$@"; do
         done
       done
       rm -rf /dev/shm/ciruela_bench_tree ;;
+    c2hcopy)  # config 2 from host memory with the two staging copy modes, alternating processes
+      for rep in $(seq 1 "${REPS:-2}"); do
+        for mode in direct nt; do
+          CIR_STAGE_COPY=$mode step "c2h_$mode" 600 python bench.py --workload config2host --steps 3 \
+            --host-gib "${HOST_GIB:-32}" --cpu-seconds 0.5 > "gpurun_out/c2hcopy_${mode}_$rep.json" \
+            2> "gpurun_out/c2hcopy_${mode}_$rep.err"
+          echo "c2h $mode rep $rep $(grep -o '"value": [0-9.]*\|"seconds_all": \[[0-9., ]*\]\|"matches_oracle": [a-z]*' "gpurun_out/c2hcopy_${mode}_$rep.json" | head -3 | tr '\n' ' ')"
+        done
+      done ;;
     cfg2sha)
       step cfg2sha 600 python bench.py --workload config2sha --steps 10 --warmup 2 \
         > gpurun_out/cfg2sha.json 2> gpurun_out/cfg2sha.err
