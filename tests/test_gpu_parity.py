@@ -749,7 +749,7 @@ def test_scan_timing_rows(gpu, tmp_path):
     rows, ph = ctx.scan_batches(), ctx.scan_phases()
     ctx.scan_timing(False)
     assert got == dirsig_oracle.scan(str(tmp_path), 32768)
-    assert len(rows) == ph["batches"] >= 10
+    assert len(rows) == ph["batches"] >= 5
     assert sum(r["blocks"] for r in rows) == sum((n + 32767) // 32768 for n in sizes)
     assert sum(r["bytes"] for r in rows) >= sum(sizes)  # + 16-B alignment of file segments
     eps = 0.05  # ms: event vs host clock
