@@ -22,6 +22,13 @@
  *   - no call changes the calling thread's current HIP device: entry points
  *     that work on other devices restore it before returning.
  *   - buffers returned through `uint8_t**` are released with cir_free().
+ *   - environment (read by the library; none is needed):
+ *       CIR_STAGE_COPY=direct  host threads fill the pinned staging slots with
+ *                              plain pread()/memcpy() instead of streaming
+ *                              (non-temporal) stores;
+ *       CIR_FOOTER=gpu         cir_init's contexts start with CIR_FOOTER_GPU;
+ *       CIR_TRACE=1            per-batch timings on stderr;
+ *       CIR_DEBUG_SPLIT=k      (tests) every opened GPU appears k times.
  */
 #ifndef CIRUELA_BLOCKHASH_H
 #define CIRUELA_BLOCKHASH_H
