@@ -1497,3 +1497,76 @@ def test_context_lifecycle_releases_device_memory(gpu, oracle):
     assert free0 - free1 < (16 << 20), (free0 - free1) >> 20
     # the pinned staging (3 x 64 MiB per context) goes back to the host too
     assert rss() - rss0 < (64 << 20), (rss() - rss0) >> 20
+
+
+def random_tree(root, rng, bs):
+    """A random tree for the scan sweep: nested directories, files whose
+    sizes sit on and around block and 128-B line edges (empty files
+    included), odd names that need escaping, executables and symlinks."""
+    names = ["a", "b c", "d\\e", "x.bin", "Ünï", "tab\tname", "z" * 40, ".hidden", "9"]
+    dirs = [root]
+    for _ in range(rng.randrange(0, 5)):
+        parent = rng.choice(dirs)
+        d = parent / ("d%d_%s" % (len(dirs), rng.choice(names)))
+        d.mkdir(exist_ok=True)
+        dirs.append(d)
+    if rng.random() < 0.3:
+        (root / "empty_dir").mkdir(exist_ok=True)
+    for k in range(rng.randrange(1, 24)):
+        d = rng.choice(dirs)
+        nb = rng.choice([0, 0, 1, 1, 2, 3, 7])
+        size = max(0, nb * bs + rng.choice([0, 0, -1, 1, 127, 128, -128, rng.randrange(-bs + 1, bs)]))
+        p = d / ("f%02d_%s" % (k, rng.choice(names)))
+        p.write_bytes(rng.randbytes(size))
+        if rng.random() < 0.2:
+            os.chmod(p, 0o755)
+    for k in range(rng.randrange(0, 3)):
+        d = rng.choice(dirs)
+        os.symlink(rng.choice(["../a", "target %d" % k, "x" * 70]), d / ("l%d" % k))
+
+
+def scan_case(gpu, seed, tmp_path, monkeypatch):
+    """One randomized end-to-end scan against the scan oracle, over the
+    scan's knobs: block size, hash type, reader threads, staging size, the
+    staging copy mode, the footer's placement and a split over 1-3 device
+    states (CIR_DEBUG_SPLIT on the one GPU)."""
+    rng = random.Random(seed)
+    bs = rng.choice([128, 1000, 4096, 32768, 65536 + 3])
+    root = tmp_path / ("t%d" % seed)
+    root.mkdir()
+    random_tree(root, rng, bs)
+    hash_name = "sha512/256" if rng.random() < 0.2 else "blake2b/256"
+    split = rng.choice([1, 1, 2, 3])
+    monkeypatch.setenv("CIR_STAGE_COPY", rng.choice(["direct", "nt"]))
+    if split > 1:
+        monkeypatch.setenv("CIR_DEBUG_SPLIT", str(split))
+    try:
+        ctx = gpu.Context(device_mask=1, staging_bytes=rng.choice([1 << 20, 3 << 20, 16 << 20]))
+    finally:
+        monkeypatch.delenv("CIR_DEBUG_SPLIT", raising=False)
+    ctx.set_footer_mode(rng.choice([ctx.FOOTER_HOST, ctx.FOOTER_GPU]))
+    ht = gpu.HashType.sha512_256() if hash_name == "sha512/256" else gpu.HashType.blake2b_256()
+    cfg = gpu.ScannerConfig.new().block_size(bs).threads(rng.choice([0, 1, 3, 4])).hash(ht)
+    cfg.add_dir(str(root), "/")
+    got = gpu.v1.scan(cfg, context=ctx)
+    want = dirsig_oracle.scan(str(root), bs, hash_name)
+    assert got == want, (seed, bs, hash_name, split)
+    assert gpu.get_hash(got) == gpu.get_hash(want)
+    ctx.close()
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_randomized_scans(gpu, tmp_path, monkeypatch, seed):
+    scan_case(gpu, 3000 + seed, tmp_path, monkeypatch)
+
+
+def test_randomized_scan_sweep(gpu, tmp_path, monkeypatch):
+    """The random scans over CIR_SCAN_SWEEP_SEEDS more seeds (0 = skipped;
+    run by hand)."""
+    n = int(os.environ.get("CIR_SCAN_SWEEP_SEEDS", "0"))
+    if n == 0:
+        pytest.skip("set CIR_SCAN_SWEEP_SEEDS to run the sweep")
+    first = int(os.environ.get("CIR_SCAN_SWEEP_FIRST", "20000"))
+    for s in range(first, first + n):
+        scan_case(gpu, s, tmp_path, monkeypatch)
+        print("scan seed %d ok" % s, flush=True)

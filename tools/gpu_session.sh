@@ -74,6 +74,10 @@ for s in "$@"; do
       step dist2 600 python bench.py --gpus 2 --dist-backend gloo --steps 5 --warmup 1 \
         --blocks "${DIST_BLOCKS:-262144}" > gpurun_out/dist2.json 2> gpurun_out/dist2.err
       cat gpurun_out/dist2.json ;;
+    dist4)  # bench.py launching four ranks itself (gloo: they share the one GPU)
+      step dist4 600 python bench.py --gpus 4 --dist-backend gloo --steps 5 --warmup 1 \
+        --blocks "${DIST_BLOCKS:-262144}" > gpurun_out/dist4.json 2> gpurun_out/dist4.err
+      cat gpurun_out/dist4.json ;;
     bench)  # the driver's command
       step bench 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench.json \
         2> gpurun_out/bench.err
