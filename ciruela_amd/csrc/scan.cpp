@@ -787,8 +787,16 @@ int cir_index_rewrite(cir_ctx* ctx, const uint8_t* in, size_t len, uint8_t** out
   static const uint8_t empty = 0;
   const int ht = idx.header.hash == dirsig::HashType::kSha512_256 ? CIR_HASH_SHA512_256
                                                                    : CIR_HASH_BLAKE2B_256;
-  int rc = cir_hash_blocks_ht(ctx, ht, blen ? (const uint8_t*)em.body_data() : &empty, &off,
-                              &blen, 1, footer);
+  int rc = CIR_OK;
+  if (ht == CIR_HASH_BLAKE2B_256 && ctx->footer == CIR_FOOTER_HOST) {
+    // the footer is one serial chain: on a host thread, as cir_scan_v1 does
+    host::Blake2b256 h;
+    h.update((const uint8_t*)em.body_data(), em.body_size());
+    h.final(footer);
+  } else {
+    rc = cir_hash_blocks_ht(ctx, ht, blen ? (const uint8_t*)em.body_data() : &empty, &off, &blen,
+                            1, footer);
+  }
   if (rc) return rc;
   *out = em.finish_malloc(footer, 32, out_len);
   if (!*out) return fail(CIR_ENOMEM, "malloc");

@@ -193,8 +193,9 @@ int cir_index_get_hash(const uint8_t* index, size_t len, uint8_t* id_out, size_t
 /* RawIndex::into_mut + MutableIndex::to_raw_data (src/cluster/download.rs:
  * 171-188, 266-319): parse, rebuild the directory tree and re-emit it in the
  * reference's order (files and links by name, then subdirectories; empty
- * directories dropped) with the footer recomputed on the GPU.  blake2b/256
- * and sha512/256 indexes (the footer is hashed with the index's hash type). */
+ * directories dropped) with the footer recomputed -- with the index's hash
+ * type: a blake2b/256 footer where cir_set_footer_mode says (a host thread
+ * by default, as in cir_scan_v1), a sha512/256 footer on the GPU. */
 int cir_index_rewrite(cir_ctx* ctx, const uint8_t* in, size_t len, uint8_t** out, size_t* out_len);
 
 /* ---- consumers of the index (host bookkeeping) ------------------------ */

@@ -482,6 +482,12 @@ def test_index_rewrite_roundtrip(gpu, small_ctx, tmp_path):
     cfg = gpu.ScannerConfig.new().add_dir(str(tmp_path), "/")
     index = gpu.v1.scan(cfg, context=small_ctx)
     assert small_ctx.index_rewrite(index) == index
+    # the footer on the GPU chain (one descriptor) gives the same bytes
+    small_ctx.set_footer_mode(small_ctx.FOOTER_GPU)
+    try:
+        assert small_ctx.index_rewrite(index) == index
+    finally:
+        small_ctx.set_footer_mode(small_ctx.FOOTER_HOST)
 
 
 def test_memory_blocks(gpu, oracle):
