@@ -16,6 +16,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdlib>
+#include <condition_variable>
 #include <thread>
 
 namespace cir {
@@ -74,6 +75,8 @@ Device::~Device() {
   (void)hipHostFree(single_h);
   (void)hipHostFree(single_out);
   (void)hipFree(single_d);
+  (void)hipHostFree(single_desc_h);
+  (void)hipFree(single_desc_d);
   if (single) (void)hipStreamDestroy(single);
   if (compute) (void)hipStreamDestroy(compute);
   if (copy) (void)hipStreamDestroy(copy);
@@ -961,19 +964,14 @@ constexpr size_t kSingleMax = 16ull << 20;
 // Up to this size the kernel reads the pinned input itself (one launch).
 constexpr size_t kSinglePull = 64ull << 10;
 
-// BlockHash::hash_bytes in one kernel launch: copy into a pinned buffer the
-// GPU reads over PCIe, launch, wait, read the digest the kernel wrote into
-// mapped host memory.
-static int single_launch(Device& d, const uint8_t* p, size_t n, uint8_t* out) {
-  std::lock_guard<std::mutex> lk(d.single_mu);
-  DeviceGuard guard;
-  CIR_HIP(hipSetDevice(d.id));
+// The single-launch input buffers (pinned device-mapped host + device
+// twin) with room for `need` bytes.  Caller holds d.single_mu with d current.
+static int ensure_single_buffers(Device& d, size_t need) {
   // each resource is checked on its own, so a failure part-way leaves the
   // rest to be created by the next call (never a launch with a null output)
   if (!d.single) CIR_HIP(hipStreamCreateWithFlags(&d.single, hipStreamNonBlocking));
   if (!d.single_out)
     CIR_HIP(hipHostMalloc(&d.single_out, 64, hipHostMallocMapped | hipHostMallocCoherent));
-  const size_t need = (n + 15) & ~(size_t)15;
   if (need > d.single_cap) {
     (void)hipHostFree(d.single_h);
     (void)hipFree(d.single_d);
@@ -990,6 +988,18 @@ static int single_launch(Device& d, const uint8_t* p, size_t n, uint8_t* out) {
     }
     d.single_cap = cap;
   }
+  return CIR_OK;
+}
+
+// BlockHash::hash_bytes in one kernel launch: copy into a pinned buffer the
+// GPU reads over PCIe, launch, wait, read the digest the kernel wrote into
+// mapped host memory.  Caller holds d.single_mu.
+static int single_launch(Device& d, const uint8_t* p, size_t n, uint8_t* out) {
+  DeviceGuard guard;
+  CIR_HIP(hipSetDevice(d.id));
+  const size_t need = (n + 15) & ~(size_t)15;
+  int rc = ensure_single_buffers(d, need);
+  if (rc) return rc;
   if (n) memcpy(d.single_h, p, n);
   // pinned host memory is device-accessible at its host address (unified
   // virtual addressing on ROCm).  Small inputs are pulled over PCIe by the
@@ -1005,14 +1015,139 @@ static int single_launch(Device& d, const uint8_t* p, size_t n, uint8_t* out) {
   return CIR_OK;
 }
 
+// Concurrent callers of cir_blake2b256 on one device, coalesced: one caller
+// at a time leads -- takes every request queued so far and hashes them as one
+// descriptor batch (a lone request goes through single_launch) -- while the
+// others wait for their digest or for the lead.  One chain's latency then
+// serves every caller that arrived meanwhile instead of one each.
+struct SingleReq {
+  const uint8_t* p;
+  size_t n;
+  uint8_t* out;
+  int rc = CIR_OK;
+  std::string err;
+  bool done = false;
+};
+
+struct SingleQueue {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<SingleReq*> pending;
+  bool leading = false;
+};
+
+// A batch of requests (total input <= kSingleBatchBytes) as descriptors on
+// the single stream.  Caller holds d.single_mu.
+static int single_batch(Device& d, const std::vector<SingleReq*>& reqs) {
+  DeviceGuard guard;
+  CIR_HIP(hipSetDevice(d.id));
+  size_t need = 0;
+  for (const SingleReq* r : reqs) need += (r->n + 15) & ~(size_t)15;
+  int rc = ensure_single_buffers(d, std::max<size_t>(need, 16));
+  if (rc) return rc;
+  const size_t m = reqs.size();
+  if (m > d.single_batch_cap) {
+    (void)hipHostFree(d.single_desc_h);
+    (void)hipFree(d.single_desc_d);
+    d.single_desc_h = nullptr;
+    d.single_desc_d = nullptr;
+    d.single_batch_cap = 0;
+    const size_t cap = std::max<size_t>(m, 256);
+    CIR_HIP(hipHostMalloc(&d.single_desc_h, cap * 48, hipHostMallocDefault));
+    const hipError_t e = hipMalloc(&d.single_desc_d, cap * 48);
+    if (e != hipSuccess) {
+      (void)hipHostFree(d.single_desc_h);
+      d.single_desc_h = nullptr;
+      return hip_fail(e, "hipMalloc(single_desc_d)");
+    }
+    d.single_batch_cap = cap;
+  }
+  // layout of both desc buffers: off[cap] (u64), len[cap] (u32), digests[cap]
+  const size_t cap = d.single_batch_cap;
+  uint64_t* h_off = (uint64_t*)d.single_desc_h;
+  uint32_t* h_len = (uint32_t*)(d.single_desc_h + 8 * cap);
+  uint8_t* h_out = d.single_desc_h + 16 * cap;
+  uint64_t pos = 0;
+  for (size_t i = 0; i < m; ++i) {
+    h_off[i] = pos;
+    h_len[i] = (uint32_t)reqs[i]->n;
+    if (reqs[i]->n) memcpy(d.single_h + pos, reqs[i]->p, reqs[i]->n);
+    pos += (reqs[i]->n + 15) & ~(size_t)15;
+  }
+  uint64_t* d_off = (uint64_t*)d.single_desc_d;
+  uint32_t* d_len = (uint32_t*)(d.single_desc_d + 8 * cap);
+  uint8_t* d_out = d.single_desc_d + 16 * cap;
+  CIR_HIP(hipMemcpyAsync(d.single_d, d.single_h, std::max<uint64_t>(pos, 16),
+                         hipMemcpyHostToDevice, d.single));
+  CIR_HIP(hipMemcpyAsync(d_off, h_off, 8 * m, hipMemcpyHostToDevice, d.single));
+  CIR_HIP(hipMemcpyAsync(d_len, h_len, 4 * m, hipMemcpyHostToDevice, d.single));
+  rc = hash_desc_ordered(d, d.single_d, d_off, d_len, m, d_out, d.single, CIR_HASH_BLAKE2B_256);
+  if (rc) return rc;
+  CIR_HIP(hipMemcpyAsync(h_out, d_out, 32 * m, hipMemcpyDeviceToHost, d.single));
+  CIR_HIP(hipStreamSynchronize(d.single));
+  for (size_t i = 0; i < m; ++i) memcpy(reqs[i]->out, h_out + 32 * i, 32);
+  return CIR_OK;
+}
+
+// Limits of one coalesced batch.
+constexpr size_t kSingleBatchBytes = 64ull << 20;
+constexpr size_t kSingleBatchMax = 4096;
+
+static int single_coalesced(Device& d, SingleQueue& q, const uint8_t* p, size_t n, uint8_t* out) {
+  SingleReq me;
+  me.p = p;
+  me.n = n;
+  me.out = out;
+  std::unique_lock<std::mutex> lk(q.mu);
+  q.pending.push_back(&me);
+  while (!me.done) {
+    if (q.leading) {
+      q.cv.wait(lk);
+      continue;
+    }
+    // lead: take what is queued (first come first), up to the batch limits
+    q.leading = true;
+    std::vector<SingleReq*> batch;
+    size_t bytes = 0, k = 0;
+    for (; k < q.pending.size() && batch.size() < kSingleBatchMax; ++k) {
+      SingleReq* r = q.pending[k];
+      if (!batch.empty() && bytes + r->n > kSingleBatchBytes) break;
+      bytes += r->n;
+      batch.push_back(r);
+    }
+    q.pending.erase(q.pending.begin(), q.pending.begin() + (std::ptrdiff_t)k);
+    lk.unlock();
+    int rc;
+    {
+      std::lock_guard<std::mutex> sl(d.single_mu);
+      rc = batch.size() == 1 ? single_launch(d, batch[0]->p, batch[0]->n, batch[0]->out)
+                             : single_batch(d, batch);
+    }
+    const std::string err = rc ? t_last_error : std::string();
+    lk.lock();
+    for (SingleReq* r : batch) {
+      r->rc = rc;
+      r->err = err;
+      r->done = true;
+    }
+    q.leading = false;
+    q.cv.notify_all();
+  }
+  lk.unlock();
+  if (me.rc) return fail(me.rc, me.err);
+  return CIR_OK;
+}
+
 static int single_shot(int ht, const uint8_t* p, size_t n, uint8_t* out) {
   if (!out || (n && !p)) return fail(CIR_EINVAL, "null pointer");
   if (n > 0xffffffffull) return fail(CIR_EINVAL, "block longer than 4 GiB");
   cir_ctx* ctx = nullptr;
   int rc = default_ctx(&ctx);
   if (rc) return rc;
-  if (ht == CIR_HASH_BLAKE2B_256 && n <= kSingleMax)
-    return single_launch(*ctx->devs[0], p, n, out);
+  if (ht == CIR_HASH_BLAKE2B_256 && n <= kSingleMax) {
+    static SingleQueue q;  // the process-default context's first device
+    return single_coalesced(*ctx->devs[0], q, p, n, out);
+  }
   static const uint8_t empty = 0;
   const uint64_t off = 0;
   const uint32_t len = (uint32_t)n;

@@ -144,6 +144,12 @@ struct Device {
   uint8_t* single_d = nullptr;
   uint8_t* single_out = nullptr;
   size_t single_cap = 0;
+  // concurrent cir_blake2b256 callers coalesced into one batch: pinned
+  // descriptors + digests (h) and their device twins (d), room for
+  // single_batch_cap requests
+  uint8_t* single_desc_h = nullptr;
+  uint8_t* single_desc_d = nullptr;
+  size_t single_batch_cap = 0;
   // per-part timing of ordered batches (cir_debug_desc_timing): one set of
   // six events per recorded batch -- ordering start / end on the caller's
   // stream, quad part start / end, lane part start / end -- under order_mu

@@ -99,10 +99,10 @@ def test_hash_bytes(gpu, oracle):
 def test_hash_bytes_from_many_threads(gpu, oracle):
     """BlockHash::hash_bytes is called per received block by the daemon's
     fetch futures (src/daemon/tracking/fetch_blocks.rs:77): eight host
-    threads hashing at once through the one default context (one single-shot
-    stream, serialised by its mutex; ctypes drops the GIL) all get their own
-    block's digest, sizes 0 .. 40 KiB across the single-shot buffer's
-    growth."""
+    threads hashing at once through the one default context (callers that
+    arrive while a launch runs are coalesced into the next one; ctypes drops
+    the GIL) all get their own block's digest, sizes 0 .. 40 KiB across the
+    single-shot buffers' growth."""
     from concurrent.futures import ThreadPoolExecutor
     rng = random.Random(77)
     blocks = [os.urandom(rng.choice([0, 1, 127, 128, 129, 4096, 32768, 40000]))
@@ -111,6 +111,32 @@ def test_hash_bytes_from_many_threads(gpu, oracle):
         got = list(ex.map(lambda b: bytes(gpu.BlockHash.hash_bytes(b)), blocks))
     for b, g in zip(blocks, got):
         assert g == oracle_digest(oracle, b), len(b)
+
+
+def test_hash_bytes_concurrent_callers_share_launches(gpu, oracle):
+    """32 threads each hashing 32 KiB blocks through the drop-in: coalesced,
+    they finish in far less than 32 x one call's time (one chain's latency
+    serves the callers that queued meanwhile), every digest correct."""
+    import time
+    from concurrent.futures import ThreadPoolExecutor
+    blk = [os.urandom(32768) for _ in range(32)]
+    want = [oracle_digest(oracle, b) for b in blk]
+    for _ in range(3):
+        bytes(gpu.BlockHash.hash_bytes(blk[0]))
+    t0 = time.perf_counter()
+    for b in blk[:8]:
+        gpu.BlockHash.hash_bytes(b)
+    one = (time.perf_counter() - t0) / 8
+    with ThreadPoolExecutor(32) as ex:
+        for _ in range(2):  # warm the batch buffers
+            list(ex.map(lambda b: bytes(gpu.BlockHash.hash_bytes(b)), blk))
+        t0 = time.perf_counter()
+        got = list(ex.map(lambda b: bytes(gpu.BlockHash.hash_bytes(b)), blk * 4))
+        both = time.perf_counter() - t0
+    assert got == want * 4
+    print("hash_bytes 32 KiB: one call %.0f us; 128 calls from 32 threads %.0f us (%.1f us/call)"
+          % (one * 1e6, both * 1e6, both * 1e6 / 128))
+    assert both < 0.5 * 128 * one, (both, one)
 
 
 @pytest.mark.parametrize("bs,nbytes", [
