@@ -7,8 +7,10 @@ latency; batched through `cir_verify_blocks` (host arena in, per-block ok
 out) the chains run side by side.  This times, for n 32 KiB blocks:
   * gpu_batch_us: one cir_verify_blocks call over the n blocks (host memory
     in and out, the process-default context), median of --calls;
-  * gpu_single_us: n calls of cir_blake2b256 (the drop-in), from the median
-    single call;
+  * gpu_single_us: n calls of cir_blake2b256 (the drop-in) one after
+    another, from the median single call;
+  * gpu_concurrent_us: the same n calls made at once from n host threads
+    (the drop-in coalesces callers that queue while a launch runs), median;
   * cpu_core_us: n blocks hashed by hashlib.blake2b(digest_size=32) on one
     host thread (CPython's C BLAKE2b: a stand-in for one core running the
     reference's `blake2` crate; not the oracle), median per block;
@@ -69,6 +71,14 @@ def main():
         ca.BlockHash.hash_bytes(one)
         single.append(time.perf_counter() - t0)
     single_blk = median(single)
+    from concurrent.futures import ThreadPoolExecutor
+    pool = ThreadPoolExecutor(256)
+    blocks = [raw[i * BS:(i + 1) * BS] for i in range(max(sizes))]
+
+    def concurrent(n):
+        futs = [pool.submit(lambda b: bytes(ca.BlockHash.hash_bytes(b)), blocks[i])
+                for i in range(n)]
+        return [f.result() for f in futs]
     rows = []
     for n in sizes:
         offs = np.arange(n, dtype=np.uint64) * BS
@@ -89,12 +99,25 @@ def main():
             call()
             ts.append(time.perf_counter() - t0)
         g = median(ts)
+        conc = None
+        if n <= 256:
+            got = concurrent(n)
+            assert b"".join(got) == want[:32 * n], n
+            tc = []
+            for _ in range(max(5, args.calls // 2)):
+                t0 = time.perf_counter()
+                concurrent(n)
+                tc.append(time.perf_counter() - t0)
+            conc = median(tc)
         rows.append({"n": n, "gpu_batch_us": round(g * 1e6, 1),
                      "gpu_batch_us_per_block": round(g * 1e6 / n, 2),
                      "gpu_single_us": round(single_blk * 1e6 * n, 1),
+                     "gpu_concurrent_us": None if conc is None else round(conc * 1e6, 1),
                      "cpu_core_us": round(cpu_blk * 1e6 * n, 1)})
-        print("n=%-5d batch %9.1f us (%7.2f us/block)  drop-in %9.1f us  one core %9.1f us"
-              % (n, g * 1e6, g * 1e6 / n, single_blk * 1e6 * n, cpu_blk * 1e6 * n), flush=True)
+        print("n=%-5d batch %9.1f us (%7.2f us/block)  drop-in %9.1f us  drop-in x n threads "
+              "%9s us  one core %9.1f us"
+              % (n, g * 1e6, g * 1e6 / n, single_blk * 1e6 * n,
+                 "-" if conc is None else "%.1f" % (conc * 1e6), cpu_blk * 1e6 * n), flush=True)
     cross = next((r["n"] for r in rows if r["gpu_batch_us"] < r["cpu_core_us"]), None)
     print(json.dumps({"block_size": BS, "cpu_core_us_per_block": round(cpu_blk * 1e6, 2),
                       "hash_bytes_us_per_call": round(single_blk * 1e6, 1),
