@@ -17,7 +17,7 @@ CLI := bin/ciruela-index
 
 SRCS_HIP := $(CSRC)/kernels.hip $(CSRC)/order.hip
 SRCS_CPP := $(CSRC)/runtime.cpp $(CSRC)/dirsig.cpp $(CSRC)/scan.cpp $(CSRC)/registry.cpp \
-            $(CSRC)/blake2b_host.cpp
+            $(CSRC)/blake2b_host.cpp $(CSRC)/sha512_host.cpp
 OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS_HIP)) \
         $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(SRCS_CPP))
 HDRS := $(wildcard $(CSRC)/*.hpp) include/ciruela_blockhash.h

@@ -84,6 +84,9 @@ def parse():
                         "prints the line skeleton with the ranks the job saw (CPU tests)")
     p.add_argument("--force-dist", action="store_true",
                    help="run the N>1 code path (process group, config 4) even at world size 1")
+    p.add_argument("--hash", choices=["blake2b", "sha512"], default="blake2b",
+                   help="config 5: the index's hash type (ciruela sync uses blake2b/256; "
+                        "sha512/256 is dir-signature's other type)")
     p.add_argument("--footer", choices=["host", "gpu", "ab"], default="host",
                    help="config 5: where the index footer is hashed (cir_set_footer_mode); "
                         "ab alternates host and gpu scans and reports both")
@@ -688,7 +691,10 @@ def run_config5(args, ca, ctx, ctx_init_s=None):
     # reader threads: the library's own choice (auto_threads: min(12, 3/4 of
     # the process's CPU share)) unless CIR_SCAN_THREADS asks
     threads = int(os.environ.get("CIR_SCAN_THREADS", "0"))
+    sha = getattr(args, "hash", "blake2b") == "sha512"
     cfg = ca.ScannerConfig.new().threads(threads).add_dir(args.tree_dir, "/")
+    if sha:
+        cfg.hash(ca.HashType.sha512_256())
     # footer placement: the library default (host), the GPU chain, or both
     # alternating in one process (--footer ab); every scan is timed per batch
     modes = {"host": ["host"], "gpu": ["gpu"], "ab": ["host", "gpu"]}[args.footer]
@@ -727,7 +733,8 @@ def run_config5(args, ca, ctx, ctx_init_s=None):
     import cpu_indexer
     lib = cpu_indexer.load()
     t0 = time.perf_counter()
-    want = cpu_indexer.index(args.tree_dir, 32768, per_gpu_share(), lib)
+    want = cpu_indexer.index(args.tree_dir, 32768, per_gpu_share(), lib,
+                             hash_name="sha512/256" if sha else "blake2b/256")
     full_s = time.perf_counter() - t0
     # 4 threads (the reference default) on a bounded sample: directories
     # d00..d03 (a tenth of the files), indexed as their own trees

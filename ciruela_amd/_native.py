@@ -112,6 +112,7 @@ _SIGS = {
                                               ctypes.c_size_t, c_sizep]),
     "cir_debug_scan_phases": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double)]),
     "cir_debug_host_blake2b256": (ctypes.c_int, [c_vp, ctypes.c_size_t, ctypes.c_size_t, c_vp]),
+    "cir_debug_host_sha512_256": (ctypes.c_int, [c_vp, ctypes.c_size_t, ctypes.c_size_t, c_vp]),
     "cir_debug_hash_uniform_dev": (ctypes.c_int, [ctypes.c_int, c_vp, ctypes.c_uint64,
                                                   ctypes.c_uint64, c_vp, c_vp]),
     "cir_fill_splitmix64_dev": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint64,

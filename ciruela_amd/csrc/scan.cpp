@@ -32,6 +32,7 @@
 
 #include "blake2b_host.hpp"
 #include "dirsig.hpp"
+#include "sha512_host.hpp"
 #include "runtime.hpp"
 
 namespace cir {
@@ -502,7 +503,8 @@ struct FooterChain {
 // Round 4, config 5 on one box (profiles/r04/footer/): see DESIGN.md 5.
 class HostFooter {
  public:
-  HostFooter() : th_([this] { run(); }) {}
+  explicit HostFooter(int ht)
+      : sha_(ht == CIR_HASH_SHA512_256 ? new host::Sha512_256 : nullptr), th_([this] { run(); }) {}
   ~HostFooter() { close(); }
   size_t fed() const { return fed_; }
   size_t feeds() const { return feeds_; }
@@ -523,7 +525,10 @@ class HostFooter {
   void finish(const dirsig::Emitter& em, uint8_t out[32]) {
     advance(em, 0);
     close();
-    st_.final(out);
+    if (sha_)
+      sha_->final(out);
+    else
+      st_.final(out);
   }
 
  private:
@@ -545,11 +550,17 @@ class HostFooter {
         take.swap(q_);
       }
       const double t0 = now_ms();
-      for (const std::string& c : take) st_.update((const uint8_t*)c.data(), c.size());
+      for (const std::string& c : take) {
+        if (sha_)
+          sha_->update((const uint8_t*)c.data(), c.size());
+        else
+          st_.update((const uint8_t*)c.data(), c.size());
+      }
       busy_ms_ += now_ms() - t0;
     }
   }
   host::Blake2b256 st_;
+  std::unique_ptr<host::Sha512_256> sha_;  // a sha512/256 index's footer
   std::mutex mu_;
   std::condition_variable cv_;
   std::vector<std::string> q_;
@@ -619,12 +630,12 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
     hdr.hash = dirsig::HashType::kSha512_256;
   else
     return fail(CIR_EINVAL, "unknown hash type");
-  // A blake2b/256 footer is hashed incrementally while the scan runs: on a
-  // host thread (CIR_FOOTER_HOST) or by the GPU chain kernel (CIR_FOOTER_GPU,
-  // quad mode); a sha512/256 footer is hashed once at the end (one lane).
-  const bool incremental = hash_type == CIR_HASH_BLAKE2B_256;
-  const bool host_footer = incremental && ctx->footer == CIR_FOOTER_HOST;
-  const bool gpu_chain = incremental && !host_footer;
+  // The footer is hashed incrementally while the scan runs: on a host
+  // thread (CIR_FOOTER_HOST, either hash type) or, for blake2b/256, by the
+  // GPU chain kernel (CIR_FOOTER_GPU, quad mode); a sha512/256 footer under
+  // CIR_FOOTER_GPU is hashed once at the end (one lane).
+  const bool host_footer = ctx->footer == CIR_FOOTER_HOST;
+  const bool gpu_chain = !host_footer && hash_type == CIR_HASH_BLAKE2B_256;
   if (threads == 0) threads = host_copy_threads(ctx->devs.size());  // auto_threads
   bool stats;
   size_t rows0;  // this scan's batches are the rows recorded from here on
@@ -663,7 +674,7 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
   CIR_HIP(hipSetDevice(dv.id));
   FooterChain chain(dv, stats);
   std::unique_ptr<HostFooter> hfoot;
-  if (host_footer) hfoot = std::make_unique<HostFooter>();
+  if (host_footer) hfoot = std::make_unique<HostFooter>(hash_type);
   int rc = gpu_chain ? chain.start() : CIR_OK;
   if (rc) return rc;
   DigestBuf digests;
@@ -788,11 +799,17 @@ int cir_index_rewrite(cir_ctx* ctx, const uint8_t* in, size_t len, uint8_t** out
   const int ht = idx.header.hash == dirsig::HashType::kSha512_256 ? CIR_HASH_SHA512_256
                                                                    : CIR_HASH_BLAKE2B_256;
   int rc = CIR_OK;
-  if (ht == CIR_HASH_BLAKE2B_256 && ctx->footer == CIR_FOOTER_HOST) {
-    // the footer is one serial chain: on a host thread, as cir_scan_v1 does
-    host::Blake2b256 h;
-    h.update((const uint8_t*)em.body_data(), em.body_size());
-    h.final(footer);
+  if (ctx->footer == CIR_FOOTER_HOST) {
+    // the footer is one serial chain: on the host, as cir_scan_v1 does
+    if (ht == CIR_HASH_SHA512_256) {
+      host::Sha512_256 h;
+      h.update((const uint8_t*)em.body_data(), em.body_size());
+      h.final(footer);
+    } else {
+      host::Blake2b256 h;
+      h.update((const uint8_t*)em.body_data(), em.body_size());
+      h.final(footer);
+    }
   } else {
     rc = cir_hash_blocks_ht(ctx, ht, blen ? (const uint8_t*)em.body_data() : &empty, &off, &blen,
                             1, footer);
@@ -842,6 +859,15 @@ int cir_debug_scan_phases(cir_ctx* ctx, double out[CIR_SCAN_PHASE_FIELDS]) {
 int cir_debug_host_blake2b256(const uint8_t* p, size_t n, size_t piece, uint8_t out[32]) {
   if (!out || (n && !p)) return fail(CIR_EINVAL, "null pointer");
   host::Blake2b256 h;
+  if (piece == 0) piece = n;
+  for (size_t off = 0; off < n; off += piece) h.update(p + off, std::min(piece, n - off));
+  h.final(out);
+  return CIR_OK;
+}
+
+int cir_debug_host_sha512_256(const uint8_t* p, size_t n, size_t piece, uint8_t out[32]) {
+  if (!out || (n && !p)) return fail(CIR_EINVAL, "null pointer");
+  host::Sha512_256 h;
   if (piece == 0) piece = n;
   for (size_t off = 0; off < n; off += piece) h.update(p + off, std::min(piece, n - off));
   h.final(out);

@@ -262,12 +262,13 @@ int cir_debug_compress_only_dev(uint64_t nlanes, uint32_t lines, uint8_t* d_out,
 int cir_debug_desc_timing(cir_ctx* ctx, int enable);
 int cir_debug_desc_times(cir_ctx* ctx, double out[5]);
 
-/* Where cir_scan_v1 hashes the footer of a blake2b/256 index (the ImageId,
- * H(every byte after the header line), src/index.rs:98-105): one serial
- * chain over the index text, ~65 B per 32 KiB block.  CIR_FOOTER_HOST (the
- * default): a host thread hashes the text as the scan emits it.
- * CIR_FOOTER_GPU: the resumable single-chain kernel (quad mode) on device 0's
- * chain stream.  Block digests are always computed on the GPU. */
+/* Where cir_scan_v1 and cir_index_rewrite hash an index's footer (the
+ * ImageId, H(every byte after the header line), src/index.rs:98-105): one
+ * serial chain over the index text, ~65 B per 32 KiB block.  CIR_FOOTER_HOST
+ * (the default): a host thread hashes the text as the scan emits it
+ * (blake2b/256 and sha512/256).  CIR_FOOTER_GPU: the resumable single-chain
+ * kernel (quad mode) on device 0's chain stream for blake2b/256, one lane at
+ * the end for sha512/256.  Block digests are always computed on the GPU. */
 enum cir_footer_mode { CIR_FOOTER_HOST = 0, CIR_FOOTER_GPU = 1 };
 int cir_set_footer_mode(cir_ctx* ctx, int mode);
 
@@ -292,9 +293,12 @@ int cir_debug_scan_timing(cir_ctx* ctx, int enable);
 int cir_debug_scan_batches(cir_ctx* ctx, double* rows, size_t max_rows, size_t* nrows);
 int cir_debug_scan_phases(cir_ctx* ctx, double out[CIR_SCAN_PHASE_FIELDS]);
 
-/* The footer's host BLAKE2b-256 fed in `piece`-byte updates (0 = one
- * update): no device involved; the CPU tests check it against the oracle. */
+/* The footer's host BLAKE2b-256 / SHA-512/256 fed in `piece`-byte updates
+ * (0 = one update): no device involved; the CPU tests check them against
+ * the oracle. */
 int cir_debug_host_blake2b256(const uint8_t* p, size_t n, size_t piece,
+                              uint8_t out[CIR_DIGEST_BYTES]);
+int cir_debug_host_sha512_256(const uint8_t* p, size_t n, size_t piece,
                               uint8_t out[CIR_DIGEST_BYTES]);
 
 /* How many whole blocks of a file of nfull x block_size bytes (plus any short

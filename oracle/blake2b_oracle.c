@@ -244,6 +244,7 @@ struct files_job {
   uint64_t bs;
   uint8_t* out;
   int err;
+  int sha; /* 1: SHA-512/256 */
   pthread_mutex_t mu;
 };
 
@@ -274,7 +275,10 @@ static void* files_worker(void* arg) {
         e = EIO;
         break;
       }
-      oracle_blake2b256(j->out + 32 * (j->first[f] + b), buf, got);
+      if (j->sha)
+        oracle_sha512_256(j->out + 32 * (j->first[f] + b), buf, got);
+      else
+        oracle_blake2b256(j->out + 32 * (j->first[f] + b), buf, got);
       ++b;
       if (got < j->bs) break;
     }
@@ -290,8 +294,8 @@ static void* files_worker(void* arg) {
   return NULL;
 }
 
-int oracle_hash_files(const char* const* paths, const uint64_t* first, const uint64_t* nblk,
-                      size_t n, uint64_t bs, uint8_t* out, int threads) {
+static int hash_files(const char* const* paths, const uint64_t* first, const uint64_t* nblk,
+                      size_t n, uint64_t bs, uint8_t* out, int threads, int sha) {
   if (bs == 0) return -EINVAL;
   if (threads < 1) threads = 1;
   if (threads > 256) threads = 256;
@@ -303,6 +307,7 @@ int oracle_hash_files(const char* const* paths, const uint64_t* first, const uin
   j.n = n;
   j.bs = bs;
   j.out = out;
+  j.sha = sha;
   pthread_mutex_init(&j.mu, NULL);
   pthread_t th[256];
   int started = 0;
@@ -312,6 +317,17 @@ int oracle_hash_files(const char* const* paths, const uint64_t* first, const uin
   for (int i = 0; i < started; ++i) pthread_join(th[i], NULL);
   pthread_mutex_destroy(&j.mu);
   return -j.err;
+}
+
+int oracle_hash_files(const char* const* paths, const uint64_t* first, const uint64_t* nblk,
+                      size_t n, uint64_t bs, uint8_t* out, int threads) {
+  return hash_files(paths, first, nblk, n, bs, out, threads, 0);
+}
+
+/* the same with HashType::sha512_256() */
+int oracle_sha_files(const char* const* paths, const uint64_t* first, const uint64_t* nblk,
+                     size_t n, uint64_t bs, uint8_t* out, int threads) {
+  return hash_files(paths, first, nblk, n, bs, out, threads, 1);
 }
 
 /* ---- SHA-512/256 (FIPS 180-4), dir-signature's HashType::sha512_256();

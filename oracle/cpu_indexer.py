@@ -21,18 +21,20 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 def load(path=None):
     lib = ctypes.CDLL(path or os.path.join(HERE, "build", "liboracle_blake2b.so"))
     vp, u64 = ctypes.c_void_p, ctypes.c_uint64
-    lib.oracle_hash_files.argtypes = [ctypes.POINTER(ctypes.c_char_p), vp, vp, ctypes.c_size_t,
-                                      u64, vp, ctypes.c_int]
+    for f in (lib.oracle_hash_files, lib.oracle_sha_files):
+        f.argtypes = [ctypes.POINTER(ctypes.c_char_p), vp, vp, ctypes.c_size_t, u64, vp,
+                      ctypes.c_int]
     lib.oracle_hash_chunks.argtypes = [vp, u64, u64, vp, ctypes.c_int]
     lib.oracle_hash_blocks.argtypes = [vp, vp, vp, ctypes.c_size_t, vp, ctypes.c_int]
     lib.oracle_splitmix64_fill.argtypes = [vp, u64, u64, u64, u64, u64]
     return lib
 
 
-def files_hasher(lib, threads):
+def files_hasher(lib, threads, hash_name="blake2b/256"):
     """files_hasher(paths, sizes, bs) -> per-file digest lists, whole files
     spread over `threads` C workers."""
     import numpy as np
+    hash_files = lib.oracle_sha_files if hash_name == "sha512/256" else lib.oracle_hash_files
 
     def run(paths, sizes, bs):
         n = len(paths)
@@ -43,8 +45,8 @@ def files_hasher(lib, threads):
         total = int(nblk.sum()) if n else 0
         out = np.zeros(32 * max(total, 1), dtype=np.uint8)
         cp = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(p) for p in paths])
-        rc = lib.oracle_hash_files(cp, first.ctypes.data, nblk.ctypes.data, n, bs,
-                                   out.ctypes.data, threads)
+        rc = hash_files(cp, first.ctypes.data, nblk.ctypes.data, n, bs, out.ctypes.data,
+                        threads)
         if rc:
             raise OSError(-rc, "oracle_hash_files: " + os.strerror(-rc))
         raw = out.tobytes()
@@ -53,7 +55,8 @@ def files_hasher(lib, threads):
     return run
 
 
-def index(root, block_size=32768, threads=4, lib=None):
+def index(root, block_size=32768, threads=4, lib=None, hash_name="blake2b/256"):
     """Index bytes of the tree at `root`, hashed on `threads` CPU workers."""
     lib = lib or load()
-    return dirsig_oracle.scan(root, block_size, files_hasher=files_hasher(lib, threads))
+    return dirsig_oracle.scan(root, block_size, hash_name,
+                              files_hasher=files_hasher(lib, threads, hash_name))

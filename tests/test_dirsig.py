@@ -88,3 +88,6 @@ def test_cpu_indexer_matches_scan_oracle(tmp_path):
     want = dirsig_oracle.scan(str(tmp_path), 4096)
     for threads in (1, 4):
         assert cpu_indexer.index(str(tmp_path), 4096, threads) == want
+    # and with dir-signature's other hash type (bench.py config 5 --hash sha512)
+    want = dirsig_oracle.scan(str(tmp_path), 4096, "sha512/256")
+    assert cpu_indexer.index(str(tmp_path), 4096, 3, hash_name="sha512/256") == want

@@ -57,3 +57,35 @@ def test_reference_fixture_rule(dirsig_example):
     idx = dirsig_example["index"].encode()
     body = idx[idx.index(b"\n") + 1:-65]
     assert host_digest(body, 7) == hashlib.blake2b(body, digest_size=32).digest()
+
+
+def host_sha_digest(data, piece=0):
+    out = ctypes.create_string_buffer(32)
+    buf = ctypes.create_string_buffer(bytes(data), max(1, len(data)))
+    _native.check(_native.lib.cir_debug_host_sha512_256(buf, len(data), piece, out))
+    return out.raw
+
+
+def test_sha512_256_footer_hasher(oracle):
+    """The sha512/256 twin (a sha512/256 index's footer, dir-signature's
+    second hash type) over lengths around the 112-byte padding edge and the
+    128-byte block, in every feed size, against the oracle and hashlib."""
+    from conftest import oracle_sha
+    rng = random.Random(12)
+    for n in [0, 1, 111, 112, 113, 127, 128, 129, 239, 240, 256, 1000, 70001]:
+        data = os.urandom(n)
+        want = oracle_sha(oracle, data)
+        assert want == hashlib.new("sha512_256", data).digest()
+        for piece in [0, 1, 64, 111, 112, 128, 129, rng.randrange(1, 500)]:
+            assert host_sha_digest(data, piece) == want, (n, piece)
+
+
+def test_sha512_256_reference_fixture(dirsig_example):
+    """The reference's own sha512/256 index (src/cluster/download.rs:357-366):
+    its footer line is this hasher's digest of its body, and its `.hidden`
+    line the digest of "Hidden\\n"."""
+    idx = dirsig_example["index"].encode()
+    body = idx[idx.index(b"\n") + 1:-65]
+    assert host_sha_digest(body, 5).hex().encode() == idx[-65:-1]
+    assert host_sha_digest(b"Hidden\n").hex() == \
+        "6d7f5f9804ee4dbc1ff7e12c7665387e0119e8ea629996c52d38b75c12ad0acf"

@@ -741,16 +741,20 @@ def test_desc_quad_mode_edges(gpu, ctx, oracle):
     assert first_bad(out.cpu().numpy(), want) is None
 
 
-@pytest.mark.parametrize("mode", ["host", "gpu"])
-def test_scan_long_index_footer(gpu, small_ctx, tmp_path, mode):
+@pytest.mark.parametrize("mode,hash_name", [("host", "blake2b/256"), ("gpu", "blake2b/256"),
+                                            ("host", "sha512/256"), ("gpu", "sha512/256")])
+def test_scan_long_index_footer(gpu, small_ctx, tmp_path, mode, hash_name):
     """An index body of several MiB (128-byte blocks): the footer is fed in
     stretches while later batches hash -- to the host thread (scan.cpp
-    HostFooter, the default) or to the device chain in >= 256 KiB pieces
-    (FooterChain) -- and must still equal H(body) (src/index.rs:98-105)."""
+    HostFooter, the default, both hash types) or, for blake2b, to the device
+    chain in >= 256 KiB pieces (FooterChain); a sha512/256 footer in GPU mode
+    is one lane at the end -- and must still equal H(body)
+    (src/index.rs:98-105)."""
     rng = random.Random(5)
     for k in range(6):
         (tmp_path / ("f%d.bin" % k)).write_bytes(rng.randbytes(rng.randrange(1 << 20, 3 << 20)))
-    cfg = gpu.ScannerConfig.new().block_size(128).add_dir(str(tmp_path), "/")
+    ht = gpu.HashType.sha512_256() if hash_name == "sha512/256" else gpu.HashType.blake2b_256()
+    cfg = gpu.ScannerConfig.new().block_size(128).hash(ht).add_dir(str(tmp_path), "/")
     small_ctx.set_footer_mode(small_ctx.FOOTER_HOST if mode == "host" else small_ctx.FOOTER_GPU)
     small_ctx.scan_timing(True)
     try:
@@ -760,9 +764,10 @@ def test_scan_long_index_footer(gpu, small_ctx, tmp_path, mode):
         small_ctx.scan_timing(False)
         small_ctx.set_footer_mode(small_ctx.FOOTER_HOST)
     assert len(got) > (4 << 20)
-    assert got == dirsig_oracle.scan(str(tmp_path), 128)
+    assert got == dirsig_oracle.scan(str(tmp_path), 128, hash_name)
     assert ph["footer_mode"] == (0 if mode == "host" else 1)
-    assert ph["footer_feeds"] >= 3 and ph["footer_busy_ms"] > 0  # fed while the scan ran
+    if mode == "host" or hash_name == "blake2b/256":
+        assert ph["footer_feeds"] >= 3 and ph["footer_busy_ms"] > 0  # fed while the scan ran
     assert ph["index_bytes"] == len(got)
 
 

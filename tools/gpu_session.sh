@@ -88,7 +88,7 @@ for s in "$@"; do
       cat gpurun_out/forcedist.json ;;
     cfg5footer)  # config 5 with the footer on the host thread and on the GPU chain, alternating
       step cfg5footer 900 python bench.py --workload config5 --footer "${FOOTER:-ab}" \
-        --steps "${STEPS:-3}" --tree-gib "${TREE_GIB:-50}" \
+        --steps "${STEPS:-3}" --tree-gib "${TREE_GIB:-50}" --hash "${HASH:-blake2b}" \
         > gpurun_out/cfg5footer.json 2> gpurun_out/cfg5footer.err
       rm -rf /dev/shm/ciruela_bench_tree
       python3 tools/cfg5_report.py gpurun_out/cfg5footer.json ;;
