@@ -744,7 +744,7 @@ def run_config5(args, ca, ctx, ctx_init_s=None):
 
     def run(th):
         for d in sample:
-            cpu_indexer.index(d, 32768, th, lib)
+            cpu_indexer.index(d, 32768, th, lib, hash_name="sha512/256" if sha else "blake2b/256")
         return sample_bytes
     if getattr(args, "no_cpu_baseline", False):
         cpu = {"skipped": "--no-cpu-baseline"}
@@ -768,6 +768,7 @@ def run_config5(args, ca, ctx, ctx_init_s=None):
                                                "a host thread" if modes[0] == "host"
                                                else "the GPU chain")},
             "footer": modes[0], "by_footer_mode": by_mode,
+            "hash_type": "sha512/256" if sha else "blake2b/256",
             # the best scan's phases: the footer's busy time (host thread, or
             # the summed k_chain_step time for the GPU chain) and its tail
             # after the last batch, and the per-batch H2D / read / wait split
