@@ -133,7 +133,7 @@ unsigned host_copy_threads(size_t ndev) {
   return (unsigned)std::min<size_t>(share, (size_t)kMaxCopyThreads * ndev);
 }
 
-bool stage_copy_nt() {  // read per call: tests switch it within one process
+bool stage_copy_nt() {  // read per API call / batch: tests switch it within one process
   const char* v = std::getenv("CIR_STAGE_COPY");
   return !(v && strcmp(v, "direct") == 0);
 }
@@ -161,8 +161,8 @@ static void stream_copy(uint8_t* dst, const uint8_t* src, size_t n) {
   _mm_sfence();
 }
 
-void copy_staged(uint8_t* dst, const uint8_t* src, size_t n) {
-  if (stage_copy_nt() && n >= 4096)
+void copy_staged(uint8_t* dst, const uint8_t* src, size_t n, bool nt) {
+  if (nt && n >= 4096)
     stream_copy(dst, src, n);
   else
     memcpy(dst, src, n);
@@ -179,8 +179,8 @@ static struct BouncePool {
   }
 } g_bounce;
 
-ssize_t pread_staged(int fd, uint8_t* dst, size_t n, off_t off) {
-  if (!stage_copy_nt() || n < 4096) return ::pread(fd, dst, n, off);
+ssize_t pread_staged(int fd, uint8_t* dst, size_t n, off_t off, bool nt) {
+  if (!nt || n < 4096) return ::pread(fd, dst, n, off);
   uint8_t* b = nullptr;
   {
     std::lock_guard<std::mutex> lk(g_bounce.mu);
@@ -502,6 +502,7 @@ static int run_blocks(cir_ctx* ctx, Device& d, const uint8_t* arena, const uint6
   CIR_HIP(hipSetDevice(d.id));
   const uint64_t cap = ctx->staging;
   const uint64_t cap_blk = std::max<uint64_t>(cap / 512, 4096);
+  const bool nt = stage_copy_nt();
   size_t next = b0;
   size_t pending_first[2] = {0, 0}, pending_n[2] = {0, 0};
   int k = 0;
@@ -536,7 +537,7 @@ static int run_blocks(cir_ctx* ctx, Device& d, const uint8_t* arena, const uint6
       const size_t base = next;
       parallel_items(n, pos, [&](size_t i0, size_t i1) {
         for (size_t i = i0; i < i1; ++i)
-          copy_staged(s.h_data + s.h_off[i], arena + off[base + i], s.h_len[i]);
+          copy_staged(s.h_data + s.h_off[i], arena + off[base + i], s.h_len[i], nt);
       });
       rc = slot_submit(d, s, std::max<uint64_t>(pos, 1), n, ht);
       if (rc) return rc;
@@ -1169,6 +1170,7 @@ int cir_hash_file_ht(cir_ctx* ctx, int hash_type, int fd, uint64_t block_size,
     return fail(CIR_EINVAL, "block_size must be in 1 .. 2^32-1");
   if (!valid_hash_type(hash_type)) return fail(CIR_EINVAL, "unknown hash type");
   std::vector<uint8_t> h;
+  const bool nt = stage_copy_nt();
   // Regular files: the bytes known to exist (st_size at the start) are read
   // with pread() by several threads per batch, then the read position moves
   // past them; beyond that (growth, pipes, sockets) plain read() to EOF,
@@ -1181,12 +1183,12 @@ int cir_hash_file_ht(cir_ctx* ctx, int hash_type, int fd, uint64_t block_size,
   if (known > 0 && ctx->devs.size() > 1 && known > block_size) {
     // several devices: split the known bytes, then make sure nothing follows
     // (a file growing meanwhile is re-hashed on one device, to its end)
-    PosReader prd = [fd, pos0](uint8_t* dst, uint64_t n, uint64_t off) -> int64_t {
+    PosReader prd = [fd, pos0, nt](uint8_t* dst, uint64_t n, uint64_t off) -> int64_t {
       const int64_t e = parallel_pieces(n, [&](uint64_t o, uint64_t len) -> int64_t {
         uint64_t got = 0;
         while (got < len) {
           const ssize_t r = pread_staged(fd, dst + o + got, len - got,
-                                         pos0 + (off_t)(off + o + got));
+                                         pos0 + (off_t)(off + o + got), nt);
           if (r < 0 && errno == EINTR) continue;
           if (r <= 0) return r < 0 ? -(int64_t)errno : (int64_t)got;
           got += (uint64_t)r;
@@ -1209,7 +1211,7 @@ int cir_hash_file_ht(cir_ctx* ctx, int hash_type, int fd, uint64_t block_size,
     }
     known = 0;  // changed while hashed: fall through to the one-device read
   }
-  Reader rd = [fd, pos0, &known, &done](uint8_t* dst, uint64_t n) -> int64_t {
+  Reader rd = [fd, pos0, nt, &known, &done](uint8_t* dst, uint64_t n) -> int64_t {
     if (done < known) {
       const uint64_t k = std::min(n, known - done);
       const uint64_t base = (uint64_t)pos0 + done;
@@ -1217,7 +1219,7 @@ int cir_hash_file_ht(cir_ctx* ctx, int hash_type, int fd, uint64_t block_size,
         uint64_t got = 0;
         while (got < len) {
           const ssize_t r = pread_staged(fd, dst + off + got, len - got,
-                                         (off_t)(base + off + got));
+                                         (off_t)(base + off + got), nt);
           if (r < 0 && errno == EINTR) continue;
           if (r < 0) return -(int64_t)errno;
           if (r == 0) break;  // truncated meanwhile
@@ -1258,10 +1260,11 @@ int cir_hash_memory_ht(cir_ctx* ctx, int hash_type, const uint8_t* data, uint64_
   if (block_size == 0 || block_size > 0xffffffffull)
     return fail(CIR_EINVAL, "block_size must be in 1 .. 2^32-1");
   if (!valid_hash_type(hash_type)) return fail(CIR_EINVAL, "unknown hash type");
+  const bool nt = stage_copy_nt();
   if (ctx->devs.size() > 1 && size > block_size) {
-    PosReader prd = [data](uint8_t* dst, uint64_t n, uint64_t off) -> int64_t {
+    PosReader prd = [data, nt](uint8_t* dst, uint64_t n, uint64_t off) -> int64_t {
       parallel_pieces(n, [&](uint64_t o, uint64_t len) -> int64_t {
-        copy_staged(dst + o, data + off + o, len);
+        copy_staged(dst + o, data + off + o, len, nt);
         return (int64_t)len;
       });
       return (int64_t)n;
@@ -1276,7 +1279,7 @@ int cir_hash_memory_ht(cir_ctx* ctx, int hash_type, const uint8_t* data, uint64_
     const uint64_t k = std::min(n, size - pos);
     const uint8_t* src = data + pos;
     parallel_pieces(k, [&](uint64_t off, uint64_t len) -> int64_t {
-      copy_staged(dst + off, src + off, len);
+      copy_staged(dst + off, src + off, len, nt);
       return (int64_t)len;
     });
     pos += k;

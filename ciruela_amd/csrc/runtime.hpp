@@ -97,9 +97,10 @@ unsigned host_copy_threads(size_t ndev);
 // upload 4.75 ms (the link's rate) and the reads faster too.
 bool stage_copy_nt();
 // n bytes into a staging slot from memory / from fd at off (pread
-// semantics: the count read, 0 at EOF, -1 with errno), in the stage mode.
-void copy_staged(uint8_t* dst, const uint8_t* src, size_t n);
-ssize_t pread_staged(int fd, uint8_t* dst, size_t n, off_t off);
+// semantics: the count read, 0 at EOF, -1 with errno), with streaming
+// stores when nt (the caller reads stage_copy_nt() once per call or batch).
+void copy_staged(uint8_t* dst, const uint8_t* src, size_t n, bool nt);
+ssize_t pread_staged(int fd, uint8_t* dst, size_t n, off_t off, bool nt);
 
 struct Device {
   int id = 0;

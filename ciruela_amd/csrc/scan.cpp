@@ -131,6 +131,7 @@ static int run_reads(const std::vector<ReadJob>& jobs, const std::vector<ScanFil
   std::atomic<int> rc{0};
   std::string err;
   std::mutex err_mu;
+  const bool nt = stage_copy_nt();
   auto worker = [&] {
     for (;;) {
       const size_t i = next.fetch_add(1);
@@ -143,7 +144,8 @@ static int run_reads(const std::vector<ReadJob>& jobs, const std::vector<ScanFil
       while (ok && got < j.len) {
         // into the pinned slot (streaming stores through a bounce buffer by
         // default: runtime.cpp pread_staged)
-        const ssize_t r = pread_staged(fd, j.dst + got, j.len - got, (off_t)(j.file_off + got));
+        const ssize_t r =
+            pread_staged(fd, j.dst + got, j.len - got, (off_t)(j.file_off + got), nt);
         if (r < 0 && errno == EINTR) continue;
         if (r <= 0) {
           ok = false;
