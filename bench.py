@@ -774,7 +774,16 @@ def run_config5(args, ca, ctx, ctx_init_s=None):
             # after the last batch, and the per-batch H2D / read / wait split
             "footer_chain_ms": best_scan["phases_ms"]["footer_busy_ms"],
             "footer_tail_ms": best_scan["phases_ms"]["footer_tail_ms"],
-            "phases_best": best_scan, "scans": scans,
+            "phases_best": best_scan,
+            # every scan, compact (the best one in full above)
+            "scans": [{"footer": sc["footer"], "seconds": sc["seconds"],
+                       "hash_loop_ms": sc["phases_ms"]["hash_loop_ms"],
+                       "footer_busy_ms": sc["phases_ms"]["footer_busy_ms"],
+                       "footer_tail_ms": sc["phases_ms"]["footer_tail_ms"],
+                       "h2d_ms_median": (sc["batches"] or {}).get("h2d_ms", {}).get("median"),
+                       "h2d_ms_p90": (sc["batches"] or {}).get("h2d_ms", {}).get("p90"),
+                       "copy_busy_frac": (sc["batches"] or {}).get("copy_busy_frac")}
+                      for sc in scans],
             "files": nfiles, "bytes": nbytes, "index_bytes": len(index),
             "image_id": ca.get_hash(index).hex(), "matches_oracle": index == want,
             "tree_gen_s": round(gen_s, 1),

@@ -8,7 +8,11 @@ nbytes = rec["bytes"]
 print("config5 value %.2f GiB/s (first %.2f), matches_oracle %s, index %.1f MB" % (
     rec["value"], rec["value_first"], rec["matches_oracle"], rec["index_bytes"] / 1e6))
 print("by footer mode: %s" % json.dumps(rec.get("by_footer_mode")))
-for sc in rec.get("scans", []):
+scans = rec.get("scans", [])
+if scans and "phases_ms" not in scans[0]:  # compact form: the best scan in full
+    print("(compact record: per-scan %s)" % json.dumps(scans))
+    scans = [rec["phases_best"]]
+for sc in scans:
     ph, b = sc["phases_ms"], sc["batches"] or {}
     print("%-4s %.3f s %6.2f GiB/s | loop %.0f tail %.1f footer busy %.0f ms feeds %d | "
           "h2d med %.2f p90 %.2f (reading %.2f n=%d, alone %s n=%d) read med %.2f wait sum %.0f "
