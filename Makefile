@@ -22,7 +22,7 @@ OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS_HIP)) \
         $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(SRCS_CPP))
 HDRS := $(wildcard $(CSRC)/*.hpp) include/ciruela_blockhash.h
 
-all: $(LIB) $(CLI) oracle
+all: $(LIB) $(CLI) build/hash_bytes_conc oracle
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -40,6 +40,12 @@ $(CLI): $(CSRC)/cli.cpp $(LIB) $(HDRS)
 	@mkdir -p bin
 	$(HIPCC) $(HOSTFLAGS) $< -o $@ -Lciruela_amd -lciruela_amd \
 	    -Wl,-rpath,'$$ORIGIN/../ciruela_amd'
+
+# concurrent hash_bytes callers from C threads (tools/hash_bytes_conc.cpp)
+build/hash_bytes_conc: tools/hash_bytes_conc.cpp $(LIB) include/ciruela_blockhash.h
+	@mkdir -p build
+	$(HIPCC) $(HOSTFLAGS) $< -o $@ -Lciruela_amd -lciruela_amd \
+	    -Wl,-rpath,'$$ORIGIN/../ciruela_amd' -lpthread
 
 oracle:
 	$(MAKE) -C oracle

@@ -119,6 +119,9 @@ for s in "$@"; do
     crossover)  # cir_verify_blocks batch vs the drop-in vs one host core, 32 KiB blocks
       step crossover 300 python tools/verify_crossover.py > gpurun_out/crossover.log 2>&1
       cat gpurun_out/crossover.log ;;
+    hbconc)  # concurrent drop-in callers from C threads
+      step hbconc 300 ./build/hash_bytes_conc 32768 64 > gpurun_out/hbconc.log 2>&1
+      cat gpurun_out/hbconc.log ;;
     latency)
       step latency 300 python tools/hash_bytes_latency.py > gpurun_out/latency.log 2>&1
       cat gpurun_out/latency.log ;;
