@@ -170,6 +170,33 @@ class Context:
         _n.check(_n.lib.cir_verify_blocks_dev(self._h, ht, d_arena, d_off, d_len, nblk,
                                               d_expected, d_digests, d_ok, d_nbad, stream))
 
+    # ---- asynchronous per-block verify (FetchBlock::poll, fetch_blocks.rs:77)
+    def verify_submit(self, data, expected, hash_type=None):
+        """Queue one block with its expected digest; returns a ticket."""
+        ht = (hash_type or HashType.blake2b_256()).code
+        if len(expected) != 32:
+            raise ValueError("expected digest must be 32 bytes")
+        ptr, keep = _buf(data) if len(data) else (ctypes.c_void_p(0), None)
+        exp = ctypes.create_string_buffer(bytes(expected), 32)
+        t = ctypes.c_uint64()
+        _n.check(_n.lib.cir_verify_submit(self._h, ht, ptr, len(data), exp, ctypes.byref(t)))
+        del keep
+        return t.value
+
+    def verify_poll(self, ticket):
+        """None while pending, else True (match) / False (mismatch)."""
+        st = ctypes.c_int()
+        _n.check(_n.lib.cir_verify_poll(self._h, ticket, ctypes.byref(st)))
+        return None if st.value == 0 else st.value == 1
+
+    def verify_wait(self, ticket):
+        ok = ctypes.c_int()
+        _n.check(_n.lib.cir_verify_wait(self._h, ticket, ctypes.byref(ok)))
+        return ok.value == 1
+
+    def verify_window(self, window_us, max_batch=4096):
+        _n.check(_n.lib.cir_verify_window(self._h, window_us, max_batch))
+
     def check_file(self, fd, block_size, expected, hash_type=None):
         ht = (hash_type or HashType.blake2b_256()).code
         if len(expected) % 32:

@@ -106,6 +106,11 @@ _SIGS = {
     "cir_debug_relay_blocks": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint64]),
     "cir_debug_desc_timing": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "cir_debug_desc_times": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double)]),
+    "cir_verify_submit": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, ctypes.c_size_t, c_vp,
+                                         ctypes.POINTER(ctypes.c_uint64)]),
+    "cir_verify_poll": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_int)]),
+    "cir_verify_wait": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_int)]),
+    "cir_verify_window": (ctypes.c_int, [c_vp, ctypes.c_uint32, ctypes.c_uint32]),
     "cir_set_footer_mode": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "cir_debug_scan_timing": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "cir_debug_scan_batches": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double),

@@ -17,7 +17,9 @@
 #include <chrono>
 #include <cstdlib>
 #include <condition_variable>
+#include <deque>
 #include <thread>
+#include <unordered_map>
 
 namespace cir {
 
@@ -1327,6 +1329,182 @@ int cir_verify_blocks(cir_ctx* ctx, int hash_type, const uint8_t* h_arena, const
     nbad += !good;
   }
   if (nbad_out) *nbad_out = nbad;
+  return CIR_OK;
+}
+
+}  // extern "C"
+
+// ---- asynchronous verify (row f2, the daemon's per-block caller) --------
+// FetchBlock::poll hashes each received block as it arrives
+// (src/daemon/tracking/fetch_blocks.rs:77).  cir_verify_submit queues one
+// block (copied) and returns at once; a worker thread per context takes
+// what has queued within av_window_us of the first waiting block (at most
+// av_max_batch blocks, one hash type per batch) and verifies it as one host
+// batch (cir_hash_blocks_ht); callers poll or wait for their ticket.  One
+// batch costs about one chain's latency whatever its size below a few
+// thousand blocks, so blocks that arrive together share it.
+namespace cir {
+
+struct AsyncVerify {
+  struct Item {
+    uint64_t ticket;
+    int ht;
+    std::vector<uint8_t> data;
+    uint8_t expected[32];
+  };
+  cir_ctx* ctx = nullptr;
+  std::mutex mu;
+  std::condition_variable cv, done_cv;
+  std::deque<Item> queue;
+  std::unordered_map<uint64_t, int> results;  // 1 match, 2 mismatch, < 0 error
+  std::unordered_map<uint64_t, std::string> errors;
+  uint64_t next_ticket = 1;
+  bool stop = false;
+  std::thread worker;
+
+  void run() {
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv.wait(lk, [&] { return stop || !queue.empty(); });
+      if (queue.empty()) return;  // stopped and drained
+      const auto deadline =
+          std::chrono::steady_clock::now() + std::chrono::microseconds(ctx->av_window_us);
+      cv.wait_until(lk, deadline, [&] { return stop || queue.size() >= ctx->av_max_batch; });
+      std::vector<Item> batch;
+      const int ht = queue.front().ht;
+      while (!queue.empty() && queue.front().ht == ht && batch.size() < ctx->av_max_batch) {
+        batch.push_back(std::move(queue.front()));
+        queue.pop_front();
+      }
+      lk.unlock();
+      std::vector<uint64_t> off(batch.size());
+      std::vector<uint32_t> len(batch.size());
+      uint64_t total = 0;
+      for (size_t i = 0; i < batch.size(); ++i) {
+        off[i] = total;
+        len[i] = (uint32_t)batch[i].data.size();
+        total += len[i];
+      }
+      std::vector<uint8_t> arena(std::max<uint64_t>(total, 1));
+      for (size_t i = 0; i < batch.size(); ++i)
+        if (len[i]) memcpy(arena.data() + off[i], batch[i].data.data(), len[i]);
+      std::vector<uint8_t> got(32 * batch.size());
+      const int rc = cir_hash_blocks_ht(ctx, ht, arena.data(), off.data(), len.data(),
+                                        batch.size(), got.data());
+      const std::string err = rc ? cir_last_error() : std::string();
+      lk.lock();
+      for (size_t i = 0; i < batch.size(); ++i) {
+        const uint64_t t = batch[i].ticket;
+        if (rc) {
+          results[t] = rc;
+          errors[t] = err;
+        } else {
+          results[t] = memcmp(got.data() + 32 * i, batch[i].expected, 32) == 0 ? 1 : 2;
+        }
+      }
+      done_cv.notify_all();
+    }
+  }
+};
+
+void AsyncVerifyDeleter::operator()(AsyncVerify* p) const {
+  {
+    std::lock_guard<std::mutex> lk(p->mu);
+    p->stop = true;
+  }
+  p->cv.notify_all();
+  if (p->worker.joinable()) p->worker.join();
+  delete p;
+}
+
+static AsyncVerify* async_verify(cir_ctx* ctx) {
+  std::lock_guard<std::mutex> lk(ctx->av_mu);
+  if (!ctx->av) {
+    AsyncVerify* a = new AsyncVerify;
+    a->ctx = ctx;
+    ctx->av.reset(a);
+    a->worker = std::thread([a] { a->run(); });
+  }
+  return ctx->av.get();
+}
+
+// A finished ticket's outcome, consumed: 1 match, 2 mismatch, < 0 error.
+static int take_result(AsyncVerify& a, uint64_t ticket, int r) {
+  a.results.erase(ticket);
+  if (r < 0) {
+    const std::string e = a.errors[ticket];
+    a.errors.erase(ticket);
+    return fail(r, e);
+  }
+  return r;
+}
+
+}  // namespace cir
+
+extern "C" {
+
+int cir_verify_submit(cir_ctx* ctx, int hash_type, const uint8_t* data, size_t n,
+                      const uint8_t expected[CIR_DIGEST_BYTES], uint64_t* ticket) {
+  if (!ctx || !ticket || !expected || (n && !data)) return fail(CIR_EINVAL, "null pointer");
+  if (!valid_hash_type(hash_type)) return fail(CIR_EINVAL, "unknown hash type");
+  if (n > 0xffffffffull) return fail(CIR_EINVAL, "block longer than 4 GiB");
+  AsyncVerify* a = async_verify(ctx);
+  AsyncVerify::Item it;
+  it.ht = hash_type;
+  it.data.assign(data, data + n);
+  memcpy(it.expected, expected, 32);
+  {
+    std::lock_guard<std::mutex> lk(a->mu);
+    it.ticket = a->next_ticket++;
+    *ticket = it.ticket;
+    a->results[it.ticket] = 0;
+    a->queue.push_back(std::move(it));
+  }
+  a->cv.notify_one();
+  return CIR_OK;
+}
+
+int cir_verify_poll(cir_ctx* ctx, uint64_t ticket, int* state) {
+  if (!ctx || !state) return fail(CIR_EINVAL, "null pointer");
+  AsyncVerify* a = async_verify(ctx);
+  std::lock_guard<std::mutex> lk(a->mu);
+  auto r = a->results.find(ticket);
+  if (r == a->results.end()) return fail(CIR_ENOTFOUND, "unknown or consumed ticket");
+  if (r->second == 0) {
+    *state = 0;
+    return CIR_OK;
+  }
+  const int v = take_result(*a, ticket, r->second);
+  if (v < 0) return v;
+  *state = v;
+  return CIR_OK;
+}
+
+int cir_verify_wait(cir_ctx* ctx, uint64_t ticket, int* ok) {
+  if (!ctx || !ok) return fail(CIR_EINVAL, "null pointer");
+  AsyncVerify* a = async_verify(ctx);
+  std::unique_lock<std::mutex> lk(a->mu);
+  auto r = a->results.find(ticket);
+  if (r == a->results.end()) return fail(CIR_ENOTFOUND, "unknown or consumed ticket");
+  // (a ticket consumed meanwhile by another caller's poll ends the wait too)
+  a->done_cv.wait(lk, [&] {
+    auto it = a->results.find(ticket);
+    return it == a->results.end() || it->second != 0;
+  });
+  r = a->results.find(ticket);
+  if (r == a->results.end()) return fail(CIR_ENOTFOUND, "ticket consumed by another caller");
+  const int v = take_result(*a, ticket, r->second);
+  if (v < 0) return v;
+  *ok = v == 1;
+  return CIR_OK;
+}
+
+int cir_verify_window(cir_ctx* ctx, uint32_t window_us, uint32_t max_batch) {
+  if (!ctx || max_batch == 0) return fail(CIR_EINVAL, "bad argument");
+  AsyncVerify* a = async_verify(ctx);
+  std::lock_guard<std::mutex> lk(a->mu);
+  ctx->av_window_us = window_us;
+  ctx->av_max_batch = max_batch;
   return CIR_OK;
 }
 

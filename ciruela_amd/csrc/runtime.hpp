@@ -191,14 +191,26 @@ struct ScanStats {
 };
 }  // namespace cir
 
+namespace cir {
+struct AsyncVerify;  // runtime.cpp: cir_verify_submit's batching worker
+struct AsyncVerifyDeleter {
+  void operator()(AsyncVerify* p) const;
+};
+}  // namespace cir
+
 struct cir_ctx {
   std::vector<std::unique_ptr<cir::Device>> devs;
   uint64_t staging = 0;
-  // where cir_scan_v1 hashes a blake2b/256 index's footer: CIR_FOOTER_HOST
-  // (one host thread beside the scan) or CIR_FOOTER_GPU (the resumable
-  // single-chain kernel on device 0's chain stream)
+  // where cir_scan_v1 hashes an index's footer: CIR_FOOTER_HOST (one host
+  // thread beside the scan) or CIR_FOOTER_GPU (the resumable single-chain
+  // kernel on device 0's chain stream)
   int footer = CIR_FOOTER_HOST;
   cir::ScanStats stats;
+  // created by the first cir_verify_submit; declared after devs, so it is
+  // stopped (its worker joined) before the devices go away
+  std::mutex av_mu;
+  std::unique_ptr<cir::AsyncVerify, cir::AsyncVerifyDeleter> av;
+  uint32_t av_window_us = 200, av_max_batch = 4096;
 };
 
 namespace cir {

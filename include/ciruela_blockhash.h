@@ -167,6 +167,23 @@ int cir_verify_blocks(cir_ctx* ctx, int hash_type, const uint8_t* h_arena, const
                       const uint32_t* len, size_t nblk, const uint8_t* expected, uint8_t* ok_out,
                       size_t* nbad_out);
 
+/* The same check one block at a time, asynchronously, for a caller that
+ * receives blocks one by one (FetchBlock::poll, fetch_blocks.rs:77):
+ * cir_verify_submit copies the block and its expected digest and returns a
+ * ticket at once; a worker thread of the context verifies what was
+ * submitted within a short window (default 200 us after the first waiting
+ * block, at most 4096 blocks, one hash type per batch) as one host batch.
+ * cir_verify_poll: *state = 0 pending, 1 match, 2 mismatch (the outcome is
+ * consumed when reported).  cir_verify_wait blocks: *ok = 1 match, 0
+ * mismatch.  A failed batch returns its error for each of its tickets; an
+ * unknown or consumed ticket is CIR_ENOTFOUND.  cir_verify_window sets the
+ * window (microseconds) and the batch cap. */
+int cir_verify_submit(cir_ctx* ctx, int hash_type, const uint8_t* data, size_t n,
+                      const uint8_t expected[CIR_DIGEST_BYTES], uint64_t* ticket);
+int cir_verify_poll(cir_ctx* ctx, uint64_t ticket, int* state);
+int cir_verify_wait(cir_ctx* ctx, uint64_t ticket, int* ok);
+int cir_verify_window(cir_ctx* ctx, uint32_t window_us, uint32_t max_batch);
+
 /* Hashes::check_file(&mut file) at image commit (src/daemon/disk/commit.rs:
  * 104; false -> Error::Checksum, :110): re-hash fd from its current offset to
  * EOF in block_size blocks; *ok_out = 1 iff the file has exactly nhash

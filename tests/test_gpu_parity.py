@@ -1607,3 +1607,78 @@ def test_randomized_scan_sweep(gpu, tmp_path, monkeypatch):
     for s in range(first, first + n):
         scan_case(gpu, s, tmp_path, monkeypatch)
         print("scan seed %d ok" % s, flush=True)
+
+
+def test_verify_async_submit_poll_wait(gpu, ctx, oracle):
+    """cir_verify_submit / poll / wait (the per-block daemon caller,
+    fetch_blocks.rs:77, batched by the library): blocks of every size class
+    (empty included) submitted from four threads, one in seven with a wrong
+    expected digest, mixed with sha512/256 blocks (batches never mix hash
+    types); every outcome right, a reported outcome is consumed, an unknown
+    ticket is NotFound."""
+    import threading
+    import time
+    n = gpu._n
+    rng = random.Random(31)
+    items = []
+    for k in range(600):
+        data = rng.randbytes(rng.choice([0, 1, 127, 128, 4096, 32768, rng.randrange(1, 70000)]))
+        sha = k % 11 == 0
+        want = oracle_sha(oracle, data) if sha else oracle_digest(oracle, data)
+        good = k % 7 != 3
+        exp = want if good else bytes([want[0] ^ 1]) + want[1:]
+        items.append((data, exp, good, sha))
+    tickets = [None] * len(items)
+
+    def submit(part):
+        for i in range(part, len(items), 4):
+            data, exp, _, sha = items[i]
+            ht = gpu.HashType.sha512_256() if sha else None
+            tickets[i] = ctx.verify_submit(data, exp, ht)
+    th = [threading.Thread(target=submit, args=(p,)) for p in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert len(set(tickets)) == len(items)
+    for (data, exp, good, sha), t in zip(items, tickets):
+        assert ctx.verify_wait(t) == good, (len(data), sha)
+    with pytest.raises(n.CiruelaError) as e:
+        ctx.verify_wait(tickets[0])  # consumed
+    assert e.value.status == n.CIR_ENOTFOUND
+    # poll: pending (None) until done, then the outcome once
+    t = ctx.verify_submit(items[5][0], items[5][1])
+    deadline = time.time() + 10
+    got = ctx.verify_poll(t)
+    while got is None and time.time() < deadline:
+        time.sleep(0.0005)
+        got = ctx.verify_poll(t)
+    assert got is True
+    with pytest.raises(n.CiruelaError):
+        ctx.verify_poll(t)
+    with pytest.raises(n.CiruelaError) as e:
+        ctx.verify_poll(123456789)
+    assert e.value.status == n.CIR_ENOTFOUND
+
+
+def test_verify_async_blocks_share_batches(gpu, oracle):
+    """256 blocks of 32 KiB submitted one by one and then waited for finish in
+    far less than 256 drop-in calls would take: the library batched them."""
+    import time
+    c = gpu.Context(device_mask=1, staging_bytes=16 << 20)
+    blk = [os.urandom(32768) for _ in range(256)]
+    want = [oracle_digest(oracle, b) for b in blk]
+    for _ in range(2):  # warm the batch path
+        for t in [c.verify_submit(b, w) for b, w in zip(blk[:64], want[:64])]:
+            assert c.verify_wait(t)
+    t0 = time.perf_counter()
+    gpu.BlockHash.hash_bytes(blk[0])
+    one = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    tickets = [c.verify_submit(b, w) for b, w in zip(blk, want)]
+    assert all(c.verify_wait(t) for t in tickets)
+    both = time.perf_counter() - t0
+    print("async verify: 256 x 32 KiB in %.2f ms (%.1f us/block); one drop-in call %.0f us"
+          % (both * 1e3, both * 1e6 / 256, one * 1e6))
+    assert both < 0.25 * 256 * one, (both, one)
+    c.close()
