@@ -206,11 +206,11 @@ struct cir_ctx {
   // kernel on device 0's chain stream)
   int footer = CIR_FOOTER_HOST;
   cir::ScanStats stats;
-  // created by the first cir_verify_submit; declared after devs, so it is
-  // stopped (its worker joined) before the devices go away
+  // cir_verify_submit's worker, created on first use; declared last, so it
+  // is stopped (its worker joined) before anything it reads goes away
+  uint32_t av_window_us = 200, av_max_batch = 4096;
   std::mutex av_mu;
   std::unique_ptr<cir::AsyncVerify, cir::AsyncVerifyDeleter> av;
-  uint32_t av_window_us = 200, av_max_batch = 4096;
 };
 
 namespace cir {
