@@ -11,6 +11,9 @@ out) the chains run side by side.  This times, for n 32 KiB blocks:
     another, from the median single call;
   * gpu_concurrent_us: the same n calls made at once from n host threads
     (the drop-in coalesces callers that queue while a launch runs), median;
+  * gpu_async_us: n blocks submitted one by one with cir_verify_submit
+    and then waited for (the library batches what arrives within its
+    window), median;
   * cpu_core_us: n blocks hashed by hashlib.blake2b(digest_size=32) on one
     host thread (CPython's C BLAKE2b: a stand-in for one core running the
     reference's `blake2` crate; not the oracle), median per block;
@@ -109,14 +112,22 @@ def main():
                 concurrent(n)
                 tc.append(time.perf_counter() - t0)
             conc = median(tc)
-        rows.append({"n": n, "gpu_batch_us": round(g * 1e6, 1),
+        asy = []
+        for _ in range(max(5, args.calls // 2)):
+            t0 = time.perf_counter()
+            tk = [ctx.verify_submit(blocks[i], want[32 * i:32 * i + 32]) for i in range(n)]
+            assert all(ctx.verify_wait(t) for t in tk)
+            asy.append(time.perf_counter() - t0)
+        a_us = median(asy)
+        rows.append({"n": n, "gpu_async_us": round(a_us * 1e6, 1),
+                     "gpu_batch_us": round(g * 1e6, 1),
                      "gpu_batch_us_per_block": round(g * 1e6 / n, 2),
                      "gpu_single_us": round(single_blk * 1e6 * n, 1),
                      "gpu_concurrent_us": None if conc is None else round(conc * 1e6, 1),
                      "cpu_core_us": round(cpu_blk * 1e6 * n, 1)})
-        print("n=%-5d batch %9.1f us (%7.2f us/block)  drop-in %9.1f us  drop-in x n threads "
-              "%9s us  one core %9.1f us"
-              % (n, g * 1e6, g * 1e6 / n, single_blk * 1e6 * n,
+        print("n=%-5d batch %9.1f us (%7.2f us/block)  async %9.1f us  drop-in %9.1f us  "
+              "drop-in x n threads %9s us  one core %9.1f us"
+              % (n, g * 1e6, g * 1e6 / n, a_us * 1e6, single_blk * 1e6 * n,
                  "-" if conc is None else "%.1f" % (conc * 1e6), cpu_blk * 1e6 * n), flush=True)
     cross = next((r["n"] for r in rows if r["gpu_batch_us"] < r["cpu_core_us"]), None)
     print(json.dumps({"block_size": BS, "cpu_core_us_per_block": round(cpu_blk * 1e6, 2),
