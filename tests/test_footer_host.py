@@ -89,3 +89,34 @@ def test_sha512_256_reference_fixture(dirsig_example):
     assert host_sha_digest(body, 5).hex().encode() == idx[-65:-1]
     assert host_sha_digest(b"Hidden\n").hex() == \
         "6d7f5f9804ee4dbc1ff7e12c7665387e0119e8ea629996c52d38b75c12ad0acf"
+
+
+def test_footer_hashers_sanitized(tmp_path):
+    """Both host hashers under AddressSanitizer + UBSan (g++ on the sources
+    alone, no device): random feeds agree with one-shot feeds, and stdin's
+    digests equal hashlib's for every piece size."""
+    import shutil
+    import subprocess
+    if shutil.which("g++") is None:
+        import pytest
+        pytest.skip("needs g++")
+    from conftest import ROOT
+    csrc = os.path.join(ROOT, "ciruela_amd", "csrc")
+    exe = str(tmp_path / "footer_hash_fuzz")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
+                    "-fno-sanitize-recover=all", "-I" + csrc,
+                    os.path.join(ROOT, "tools", "footer_hash_fuzz.cpp"),
+                    os.path.join(csrc, "blake2b_host.cpp"), os.path.join(csrc, "sha512_host.cpp"),
+                    "-o", exe], check=True)
+    rng = random.Random(5)
+    for n, piece in [(0, 0), (1, 1), (111, 7), (112, 0), (128, 128), (129, 64), (4096, 1000),
+                     (200000, 256 << 10), (70001, rng.randrange(1, 5000))]:
+        data = os.urandom(n)
+        p = subprocess.run([exe, "300", str(piece)], input=data, capture_output=True,
+                           timeout=120)
+        assert p.returncode == 0, p.stderr[-3000:]
+        out = p.stdout.decode().split("\n")
+        b2, sh = out[0].split()
+        assert b2 == hashlib.blake2b(data, digest_size=32).hexdigest(), n
+        assert sh == hashlib.new("sha512_256", data).hexdigest(), n
+        assert "no sanitizer report" in p.stdout.decode()
