@@ -1682,3 +1682,70 @@ def test_verify_async_blocks_share_batches(gpu, oracle):
           % (both * 1e3, both * 1e6 / 256, one * 1e6))
     assert both < 0.25 * 256 * one, (both, one)
     c.close()
+
+
+def host_case(gpu, oracle, seed, tmp_path, monkeypatch):
+    """One randomized round of the host-memory entry points against the
+    oracle, over the staging knobs: staging size, copy mode, 1-3 device
+    states.  Descriptor batches (cir_hash_blocks, both hash types), batch
+    and asynchronous verify with some wrong digests, an in-memory file
+    (cir_hash_memory) and a file read from an offset (cir_hash_file)."""
+    rng = random.Random(seed)
+    monkeypatch.setenv("CIR_STAGE_COPY", rng.choice(["direct", "nt"]))
+    split = rng.choice([1, 1, 2, 3])
+    if split > 1:
+        monkeypatch.setenv("CIR_DEBUG_SPLIT", str(split))
+    try:
+        c = gpu.Context(device_mask=1, staging_bytes=rng.choice([1 << 20, 5 << 20, 32 << 20]))
+    finally:
+        monkeypatch.delenv("CIR_DEBUG_SPLIT", raising=False)
+    arena = rng.randbytes(rng.choice([1 << 16, 3 << 20, 9 << 20]))
+    n = rng.choice([1, 5, 300, 2000])
+    lens = [rng.choice([0, 1, 127, 128, 129, 4096, 32768, rng.randrange(0, 200000)])
+            for _ in range(n)]
+    lens = [min(ln, len(arena)) for ln in lens]
+    offs = [rng.randrange(0, len(arena) - ln + 1) for ln in lens]
+    sha = rng.random() < 0.25
+    ht = gpu.HashType.sha512_256() if sha else None
+    h = (lambda b: oracle_sha(oracle, b)) if sha else (lambda b: oracle_digest(oracle, b))
+    want = [h(arena[o:o + ln]) for o, ln in zip(offs, lens)]
+    assert c.hash_blocks(arena, offs, lens, ht) == b"".join(want), seed
+    bad = {i for i in range(n) if rng.random() < 0.1}
+    exp = b"".join(w if i not in bad else bytes([w[0] ^ 0x80]) + w[1:]
+                   for i, w in enumerate(want))
+    assert c.verify_blocks(arena, offs, lens, exp, ht) == [i not in bad for i in range(n)]
+    k = min(n, 40)
+    tickets = [c.verify_submit(arena[offs[i]:offs[i] + lens[i]], exp[32 * i:32 * i + 32], ht)
+               for i in range(k)]
+    assert [c.verify_wait(t) for t in tickets] == [i not in bad for i in range(k)]
+    bs = rng.choice([128, 1000, 4096, 32768, 65536 + 3])
+    size = rng.randrange(0, len(arena) + 1)
+    blob = arena[:size]
+    chunks = b"".join(h(blob[i:i + bs]) for i in range(0, size, bs))
+    assert c.hash_memory(blob, bs, ht) == chunks, seed
+    p = tmp_path / ("f%d.bin" % seed)
+    p.write_bytes(blob)
+    skip = rng.randrange(0, size + 1)
+    with open(p, "rb") as f:
+        f.seek(skip)
+        got_size, hashes = c.hash_file(f.fileno(), bs, ht)
+    tail = blob[skip:]
+    assert got_size == len(tail)
+    assert hashes == b"".join(h(tail[i:i + bs]) for i in range(0, len(tail), bs)), seed
+    c.close()
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_randomized_host_paths(gpu, oracle, tmp_path, monkeypatch, seed):
+    host_case(gpu, oracle, 4000 + seed, tmp_path, monkeypatch)
+
+
+def test_randomized_host_sweep(gpu, oracle, tmp_path, monkeypatch):
+    """The host-path cases over CIR_HOST_SWEEP_SEEDS more seeds (0 = skipped)."""
+    n = int(os.environ.get("CIR_HOST_SWEEP_SEEDS", "0"))
+    if n == 0:
+        pytest.skip("set CIR_HOST_SWEEP_SEEDS to run the sweep")
+    first = int(os.environ.get("CIR_HOST_SWEEP_FIRST", "30000"))
+    for s in range(first, first + n):
+        host_case(gpu, oracle, s, tmp_path, monkeypatch)
+        print("host seed %d ok" % s, flush=True)
