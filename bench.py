@@ -897,6 +897,10 @@ def run_config5_leg(args, ca, ctx, dev, stream):
             return {"skipped": "MemAvailable %.1f GiB, the %.0f GiB tmpfs tree needs %.0f + 8"
                                % (avail, args.tree_gib, need), "matches_oracle": None}
     try:
+        try:
+            make_tree(args.tree_dir, args.tree_gib)
+        except OSError as e:  # the box's tmpfs, not the indexer: a skip, not a parity failure
+            return {"skipped": "could not write the tree: %s" % e, "matches_oracle": None}
         return run_config5(args, ca, ctx)
     finally:
         shutil.rmtree(args.tree_dir, ignore_errors=True)

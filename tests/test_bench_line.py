@@ -109,3 +109,16 @@ def test_config5_leg_checks_ram_and_reuses_a_complete_tree(tmp_path, monkeypatch
     monkeypatch.setattr(bench, "run_config5", lambda a, ca, ctx: called.append(1) or {"x": 1})
     assert bench.run_config5_leg(args, None, None, None, None) == {"x": 1} and called
     assert not os.path.exists(args.tree_dir)  # removed afterwards
+
+
+def test_config5_leg_tree_write_failure_is_a_skip(tmp_path, monkeypatch):
+    """A tree the box cannot write (tmpfs full, permissions) skips the leg
+    with the reason instead of reporting a parity failure."""
+    args = argparse.Namespace(tree_dir=str(tmp_path / "tree"), tree_gib=0.01, steps=1)
+    monkeypatch.setattr(bench, "mem_available_gib", lambda: 1e6)
+
+    def boom(root, gib):
+        raise OSError(28, "No space left on device")
+    monkeypatch.setattr(bench, "make_tree", boom)
+    rec = bench.run_config5_leg(args, None, None, None, None)
+    assert "No space left" in rec["skipped"] and rec["matches_oracle"] is None
