@@ -567,12 +567,16 @@ def run_config2sha(args, ca, ctx, dev, stream):
 
 
 def make_tree(root, gib, file_mib=32, ndirs=40, seed=0x5EED0005):
-    """Config 5 tree: files of file_mib MiB in ndirs directories."""
+    """Config 5 tree: files of file_mib MiB in ndirs directories.  A complete
+    tree of this size is reused; anything else at root (a tree of another
+    size, a partial one) is removed first, so the scan sees exactly nfiles."""
+    import shutil
     import numpy as np
     nfiles = int(gib * 1024 // file_mib)
     done = os.path.join(root, ".complete-%d-%d" % (nfiles, file_mib))
     if os.path.exists(done):
         return nfiles
+    shutil.rmtree(root, ignore_errors=True)
     os.makedirs(root, exist_ok=True)
     rng = np.random.default_rng(seed)
     base = rng.integers(0, 1 << 63, size=file_mib * (1 << 20) // 8, dtype=np.uint64)

@@ -188,18 +188,22 @@ struct DigestBuf {
 // while the previous batch uploads and hashes.
 using Progress = std::function<int(uint64_t done_blk)>;
 
-// Blocks [b0, b1) of the global block order on device d (files stay in
-// order; a range may start or end inside a file).  done(n) is called after
-// each batch with the number of blocks of the range finished so far (a
-// prefix of the range: the slots retire in submission order).
+// The block ranges `ranges` (each [b0, b1) of the global block order, in
+// increasing order; a range may start or end inside a file) on device d, one
+// pipeline across all of them (a batch never spans two ranges).  done(r, n)
+// is called after each batch with the range's index and the number of its
+// blocks finished so far (a prefix of the range: the slots retire in
+// submission order).
 // With `scan_t0` >= 0 (cir_debug_scan_timing on) every batch is timed and
 // appended to ctx->stats as a row (include/ciruela_blockhash.h), times in ms
 // since scan_t0 on the host clock; the device's copy stream gets a reference
 // event at the start that maps its HIP event times onto that clock.
+using BlockRanges = std::vector<std::pair<uint64_t, uint64_t>>;
 static int hash_range(cir_ctx* ctx, Device& d, size_t di, const std::vector<ScanFile>& files,
                       uint64_t bs, unsigned threads, int ht, DigestBuf& digests,
-                      uint64_t b0, uint64_t b1, const std::function<int(uint64_t)>& done,
-                      double scan_t0) {
+                      const BlockRanges& ranges,
+                      const std::function<int(size_t, uint64_t)>& done, double scan_t0) {
+  if (ranges.empty()) return CIR_OK;
   std::lock_guard<std::mutex> lk(d.mu);
   DeviceGuard guard;
   CIR_HIP(hipSetDevice(d.id));
@@ -218,14 +222,25 @@ static int hash_range(cir_ctx* ctx, Device& d, size_t di, const std::vector<Scan
   std::vector<std::array<double, kScanBatchFields>> rows;
   const uint64_t cap = std::max<uint64_t>(ctx->staging, bs + 16);
   const uint64_t cap_blk = std::max<uint64_t>(cap / 512, 4096);
-  // first file with a block >= b0
-  size_t fi = std::upper_bound(files.begin(), files.end(), b0,
-                               [](uint64_t b, const ScanFile& f) { return b < f.first_blk; }) -
-              files.begin();
-  fi = fi ? fi - 1 : 0;
-  uint64_t fblk = b0 > files[fi].first_blk ? b0 - files[fi].first_blk : 0;  // next block within it
+  size_t ri = 0;  // the range being packed
+  uint64_t b0 = 0, b1 = 0;
+  size_t fi = 0;
+  uint64_t fblk = 0;  // next block within files[fi]
+  auto start_range = [&](size_t r) {
+    ri = r;
+    b0 = ranges[r].first;
+    b1 = ranges[r].second;
+    // the last file whose first block is <= b0 (empty files share first_blk)
+    fi = std::upper_bound(files.begin(), files.end(), b0,
+                          [](uint64_t b, const ScanFile& f) { return b < f.first_blk; }) -
+         files.begin();
+    fi = fi ? fi - 1 : 0;
+    fblk = b0 > files[fi].first_blk ? b0 - files[fi].first_blk : 0;
+  };
+  start_range(0);
   constexpr int kS = Device::kSlots;
   uint64_t pending_first[kS] = {}, pending_n[kS] = {};
+  size_t pending_range[kS] = {};
   double pending_row[kS][6] = {};  // bytes, blocks, wait, read start, read end
   int k = 0;
   auto busy = [&] {
@@ -233,12 +248,21 @@ static int hash_range(cir_ctx* ctx, Device& d, size_t di, const std::vector<Scan
       if (s.busy) return true;
     return false;
   };
-  auto more = [&] {
+  // blocks left in the current range
+  auto more_here = [&] {
     while (fi < files.size() && fblk * bs >= files[fi].size) {
       ++fi;
       fblk = 0;
     }
     return fi < files.size() && files[fi].first_blk + fblk < b1;
+  };
+  // blocks left in this or a later range (moves on to the next range)
+  auto more = [&] {
+    while (!more_here()) {
+      if (ri + 1 >= ranges.size()) return false;
+      start_range(ri + 1);
+    }
+    return true;
   };
   while (more() || busy()) {
     Slot& s = d.slot[k];
@@ -264,7 +288,8 @@ static int hash_range(cir_ctx* ctx, Device& d, size_t di, const std::vector<Scan
                         ref_ms + e[2], ref_ms + e[3]});
       }
       memcpy(digests.data() + 32 * pending_first[k], s.h_out, 32 * pending_n[k]);
-      rc = done(pending_first[k] + pending_n[k] - b0);
+      const size_t pr = pending_range[k];
+      rc = done(pr, pending_first[k] + pending_n[k] - ranges[pr].first);
       if (rc) return rc;
     }
     const bool clock = trace_on() || stats;
@@ -275,7 +300,7 @@ static int hash_range(cir_ctx* ctx, Device& d, size_t di, const std::vector<Scan
       std::vector<ReadJob> jobs;
       uint64_t pos = 0, n = 0;
       const uint64_t first = files[fi].first_blk + fblk;
-      while (more() && n < cap_blk) {
+      while (more_here() && n < cap_blk) {
         const ScanFile& f = files[fi];
         const uint64_t left_blk = std::min<uint64_t>((f.size + bs - 1) / bs - fblk,
                                                      b1 - (f.first_blk + fblk));
@@ -310,6 +335,7 @@ static int hash_range(cir_ctx* ctx, Device& d, size_t di, const std::vector<Scan
                 pos / 1e6 / std::max(t_read1 - t_read0, 1e-3));
       pending_first[k] = first;
       pending_n[k] = n;
+      pending_range[k] = ri;
       if (stats) {
         pending_row[k][0] = (double)pos;
         pending_row[k][1] = (double)n;
@@ -331,11 +357,15 @@ static int hash_range(cir_ctx* ctx, Device& d, size_t di, const std::vector<Scan
 // Batches are packed into the staging slots of a device (file segments
 // 16-byte aligned, one descriptor per block) by `threads` reader threads
 // while the previous batches upload and hash.  With several devices in the
-// context the global block order is split into one contiguous range per
-// device (equal block counts), each driven by its own thread
-// with threads / ndev readers; progress(n) then reports the prefix of the
-// global order that is complete, called under a lock on device 0's
-// current-device setting (the emitter feeds device 0's footer chain).
+// context the global block order is cut into stripes of one staging batch's
+// worth of whole blocks, dealt round-robin to the devices (SURVEY.md 8e's
+// range split, interleaved), each device driven by its own thread with
+// threads / ndev readers; progress(n) reports the prefix of the global order
+// that is complete -- with interleaved stripes it advances steadily while the
+// devices work, so the emitter and the footer keep streaming (one contiguous
+// range per device held the whole index back until device 0's range had
+// finished, and hashed most of the footer after the last batch) -- called
+// under a lock with device 0 current.
 static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, unsigned threads,
                       int ht, DigestBuf& digests, const Progress& progress,
                       double scan_t0) {
@@ -351,23 +381,36 @@ static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, u
   if (nblk_total == 0) return CIR_OK;
   const size_t nd = std::min<size_t>(ctx->devs.size(), nblk_total);
   if (nd <= 1)
-    return hash_range(ctx, *ctx->devs[0], 0, files, bs, threads, ht, digests, 0, nblk_total,
-                      progress, scan_t0);
-  std::vector<uint64_t> lo(nd), hi(nd), got(nd, 0);
-  for (size_t i = 0; i < nd; ++i) {
-    lo[i] = nblk_total * i / nd;
-    hi[i] = nblk_total * (i + 1) / nd;
+    return hash_range(ctx, *ctx->devs[0], 0, files, bs, threads, ht, digests,
+                      {{0, nblk_total}},
+                      [&](size_t, uint64_t n) { return progress(n); }, scan_t0);
+  uint64_t stripe = std::max<uint64_t>(1, ctx->staging / bs);
+  if (const char* e = getenv("CIR_DEBUG_STRIPE_BLOCKS"))  // tests: stripes of a few blocks
+    if (atoll(e) > 0) stripe = (uint64_t)atoll(e);
+  const size_t nstripes = (size_t)((nblk_total + stripe - 1) / stripe);
+  std::vector<BlockRanges> dev_ranges(nd);
+  std::vector<std::vector<size_t>> global_index(nd);  // (device, range) -> stripe
+  for (size_t st = 0; st < nstripes; ++st) {
+    const size_t i = st % nd;
+    dev_ranges[i].push_back({st * stripe, std::min<uint64_t>((st + 1) * stripe, nblk_total)});
+    global_index[i].push_back(st);
   }
+  std::vector<uint64_t> got(nstripes, 0);
+  size_t first_open = 0;  // first stripe not yet complete
   std::mutex mu;
   const int dev0 = ctx->devs[0]->id;
-  auto done = [&](size_t i, uint64_t n) -> int {
+  auto done = [&](size_t i, size_t r, uint64_t n) -> int {
     std::lock_guard<std::mutex> lk(mu);
-    got[i] = n;
-    uint64_t prefix = 0;
-    for (size_t j = 0; j < nd; ++j) {
-      prefix = lo[j] + got[j];
-      if (got[j] < hi[j] - lo[j]) break;
-    }
+    const size_t st = global_index[i][r];
+    got[st] = n;
+    const uint64_t before = first_open < nstripes ? first_open * stripe + got[first_open]
+                                                  : nblk_total;
+    while (first_open < nstripes &&
+           got[first_open] == std::min<uint64_t>(stripe, nblk_total - first_open * stripe))
+      ++first_open;
+    const uint64_t prefix = first_open < nstripes ? first_open * stripe + got[first_open]
+                                                  : nblk_total;
+    if (prefix == before) return CIR_OK;  // this batch did not extend the prefix
     int cur = 0;
     CIR_HIP(hipGetDevice(&cur));
     CIR_HIP(hipSetDevice(dev0));
@@ -381,8 +424,8 @@ static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, u
   std::vector<std::thread> th;
   for (size_t i = 0; i < nd; ++i)
     th.emplace_back([&, i] {
-      rc[i] = hash_range(ctx, *ctx->devs[i], i, files, bs, per, ht, digests, lo[i], hi[i],
-                         [&, i](uint64_t n) { return done(i, n); }, scan_t0);
+      rc[i] = hash_range(ctx, *ctx->devs[i], i, files, bs, per, ht, digests, dev_ranges[i],
+                         [&, i](size_t r, uint64_t n) { return done(i, r, n); }, scan_t0);
       if (rc[i]) err[i] = cir_last_error();
     });
   for (auto& t : th) t.join();
@@ -391,7 +434,6 @@ static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, u
   CIR_HIP(hipSetDevice(dev0));
   return CIR_OK;
 }
-
 
 // ---- incremental footer ---------------------------------------------------
 // The footer is H(index body): one sequential chain over the whole body.  The

@@ -29,6 +29,9 @@
  *       CIR_FOOTER=gpu         cir_init's contexts start with CIR_FOOTER_GPU;
  *       CIR_TRACE=1            per-batch timings on stderr;
  *       CIR_DEBUG_SPLIT=k      (tests) every opened GPU appears k times.
+ *       CIR_DEBUG_STRIPE_BLOCKS=n  (tests) a scan over several devices deals
+ *                              stripes of n blocks (default: one staging
+ *                              slot of whole blocks) round-robin to them.
  */
 #ifndef CIRUELA_BLOCKHASH_H
 #define CIRUELA_BLOCKHASH_H

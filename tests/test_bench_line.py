@@ -122,3 +122,19 @@ def test_config5_leg_tree_write_failure_is_a_skip(tmp_path, monkeypatch):
     monkeypatch.setattr(bench, "make_tree", boom)
     rec = bench.run_config5_leg(args, None, None, None, None)
     assert "No space left" in rec["skipped"] and rec["matches_oracle"] is None
+
+
+def test_make_tree_replaces_a_tree_of_another_size(tmp_path):
+    """A tree of another size left at --tree-dir (an earlier run with another
+    --tree-gib) is removed before the new one is written, so the scan indexes
+    exactly the files its byte count assumes."""
+    root = str(tmp_path / "tree")
+
+    def files():
+        return sorted(f for _, _, fs in os.walk(root) for f in fs if not f.startswith("."))
+    assert bench.make_tree(root, 4 / 1024, file_mib=1, ndirs=2) == 4
+    assert len(files()) == 4
+    assert bench.make_tree(root, 2 / 1024, file_mib=1, ndirs=2) == 2
+    assert files() == ["f00000.bin", "f00001.bin"]
+    assert bench.make_tree(root, 2 / 1024, file_mib=1, ndirs=2) == 2  # complete: reused
+    assert os.listdir(root).count(".complete-2-1") == 1

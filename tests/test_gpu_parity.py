@@ -916,10 +916,12 @@ def test_hash_file_parallel_reads_offset_and_pipe(ctx, oracle, tmp_path, copy, m
 
 def test_multi_device_split_paths(gpu, oracle, tmp_path):
     """The host paths' multi-device splits (one contiguous
-    block range per device, one thread each), run on one GPU through
-    CIR_DEBUG_SPLIT=3 (the GPU appears as three independent device states):
-    hash_memory, hash_file from an offset, hash_blocks, and a directory scan
-    whose footer chain is fed from the device threads."""
+    block range per device for hash_memory / hash_file / hash_blocks, stripes
+    dealt round-robin for a scan; one thread per device), run on one GPU
+    through CIR_DEBUG_SPLIT=3 (the GPU appears as three independent device
+    states): hash_memory, hash_file from an offset, hash_blocks, and a
+    directory scan whose footer is fed from the device threads, with the
+    default stripes and with stripes of 3 blocks."""
     os.environ["CIR_DEBUG_SPLIT"] = "3"
     try:
         ctx = gpu.Context(device_mask=1, staging_bytes=1 << 20)
@@ -955,6 +957,11 @@ def test_multi_device_split_paths(gpu, oracle, tmp_path):
         for mode in (ctx.FOOTER_HOST, ctx.FOOTER_GPU):
             ctx.set_footer_mode(mode)
             assert gpu.v1.scan(cfg, context=ctx) == want, (block_size, mode)
+            os.environ["CIR_DEBUG_STRIPE_BLOCKS"] = "3"
+            try:
+                assert gpu.v1.scan(cfg, context=ctx) == want, (block_size, mode, 3)
+            finally:
+                del os.environ["CIR_DEBUG_STRIPE_BLOCKS"]
 
 
 def test_error_paths_are_codes_not_aborts(gpu, small_ctx, tmp_path):
@@ -1577,6 +1584,9 @@ def scan_case(gpu, seed, tmp_path, monkeypatch):
     monkeypatch.setenv("CIR_STAGE_COPY", rng.choice(["direct", "nt"]))
     if split > 1:
         monkeypatch.setenv("CIR_DEBUG_SPLIT", str(split))
+        # the scan deals stripes of blocks round-robin to the devices: make
+        # them a few blocks long so small trees cross many stripe edges
+        monkeypatch.setenv("CIR_DEBUG_STRIPE_BLOCKS", str(rng.choice([0, 1, 2, 5])))
     try:
         ctx = gpu.Context(device_mask=1, staging_bytes=rng.choice([1 << 20, 3 << 20, 16 << 20]))
     finally:
@@ -1586,6 +1596,7 @@ def scan_case(gpu, seed, tmp_path, monkeypatch):
     cfg = gpu.ScannerConfig.new().block_size(bs).threads(rng.choice([0, 1, 3, 4])).hash(ht)
     cfg.add_dir(str(root), "/")
     got = gpu.v1.scan(cfg, context=ctx)
+    monkeypatch.delenv("CIR_DEBUG_STRIPE_BLOCKS", raising=False)
     want = dirsig_oracle.scan(str(root), bs, hash_name)
     assert got == want, (seed, bs, hash_name, split)
     assert gpu.get_hash(got) == gpu.get_hash(want)
