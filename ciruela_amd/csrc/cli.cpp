@@ -149,12 +149,23 @@ int main(int argc, char** argv) {
   for (const Job& j : jobs) inputs.push_back(j.src);
   cir_ctx* ctx = nullptr;
   const uint64_t staging = staging_for(inputs);
-  if (const char* t = getenv("CIR_TRACE"))
-    if (*t && strcmp(t, "0") != 0)
-      fprintf(stderr, "ciruela-index: staging %llu bytes per slot (0 = library default)\n",
-              (unsigned long long)staging);
+  const char* tv = getenv("CIR_TRACE");
+  const bool trace = tv && *tv && strcmp(tv, "0") != 0;
+  auto ms_since = [](std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+  };
+  if (trace) {
+    fprintf(stderr, "ciruela-index: staging %llu bytes per slot (0 = library default)\n",
+            (unsigned long long)staging);
+    // the HIP runtime's own start-up (device discovery), apart from cir_init
+    const auto t0 = std::chrono::steady_clock::now();
+    const int n = cir_device_count();
+    fprintf(stderr, "ciruela-index: HIP runtime start %.1f ms (%d devices)\n", ms_since(t0), n);
+  }
+  const auto t_init = std::chrono::steady_clock::now();
   int rc = cir_init(&ctx, 0, staging);
   if (rc) return die(rc, "cir_init");
+  if (trace) fprintf(stderr, "ciruela-index: cir_init %.1f ms\n", ms_since(t_init));
   if (cmd == "hash") {
     for (const std::string& f : files) {
       const int fd = open(f.c_str(), O_RDONLY);
@@ -217,6 +228,8 @@ int main(int argc, char** argv) {
     usage();
     return 2;
   }
+  const auto t_destroy = std::chrono::steady_clock::now();
   cir_destroy(ctx);
+  if (trace) fprintf(stderr, "ciruela-index: cir_destroy %.1f ms\n", ms_since(t_destroy));
   return 0;
 }

@@ -713,6 +713,16 @@ static int export_hashes(const std::vector<uint8_t>& h, uint8_t** out, size_t* n
 //   * one small upload on the staging and on the footer-chain stream.
 // Caller holds a DeviceGuard.
 static int init_device(Device& d, uint64_t staging, bool lazy) {
+  // CIR_TRACE: each step's ms on stderr (the one-shot CLI's start-up budget)
+  const bool tr = trace_enabled();
+  auto t = std::chrono::steady_clock::now();
+  auto step = [&](const char* what) {
+    if (!tr) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "cir_init dev %d: %s %.2f ms\n", d.id, what,
+            std::chrono::duration<double, std::milli>(now - t).count());
+    t = now;
+  };
   CIR_HIP(hipSetDevice(d.id));
   CIR_HIP(hipStreamCreateWithFlags(&d.compute, hipStreamNonBlocking));
   CIR_HIP(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
@@ -726,21 +736,26 @@ static int init_device(Device& d, uint64_t staging, bool lazy) {
     if (rc == CIR_OK) rc = ensure_relay(d);
     if (rc) return rc;
   }
+  step("streams, events, relay scratch");
   const uint64_t cap_blk = std::max<uint64_t>(staging / 512, 4096);
   const uint64_t slot_bytes = lazy ? (64ull << 10) : std::max<uint64_t>(staging, 16);
   for (int k = 0; k < (lazy ? 2 : Device::kSlots); ++k) {
     const int rc = d.ensure_slot(d.slot[k], slot_bytes, lazy ? 4096 : cap_blk);
     if (rc) return rc;
   }
+  step("staging slots");
   Slot& s = d.slot[0];
   CIR_HIP(hipMemsetAsync(s.d_data, 0, 4096, d.compute));
   CIR_HIP(hipMemsetAsync(s.d_off, 0, 8, d.compute));
   CIR_HIP(hipMemsetAsync(s.d_len, 0, 4, d.compute));
   CIR_HIP(dev::launch_chunks(s.d_data, 4096, 1024, s.d_out, d.compute));
+  CIR_HIP(hipStreamSynchronize(d.compute));
+  step("first kernel (code object load)");
   const int rc = hash_desc_ordered(d, s.d_data, s.d_off, s.d_len, cap_blk, s.d_out, d.compute,
                                    CIR_HASH_BLAKE2B_256, /*warm_only=*/true);
   if (rc) return rc;
   CIR_HIP(hipStreamSynchronize(d.compute));
+  step("ordered descriptor batch");
   // the process's first host->device copy on a stream takes 7-11 ms more
   // than the next (profiles/r03_s2/cli/: a 10 MiB batch's upload 7.7-10.7 ms
   // in a fresh CLI process, ~0.2 ms later): pay it here for the staging and
@@ -751,6 +766,7 @@ static int init_device(Device& d, uint64_t staging, bool lazy) {
                          d.chain));
   CIR_HIP(hipStreamSynchronize(d.copy));
   CIR_HIP(hipStreamSynchronize(d.chain));
+  step("first uploads");
   return CIR_OK;
 }
 
