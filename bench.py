@@ -90,6 +90,10 @@ def parse():
     p.add_argument("--footer", choices=["host", "gpu", "ab"], default="host",
                    help="config 5: where the index footer is hashed (cir_set_footer_mode); "
                         "ab alternates host and gpu scans and reports both")
+    p.add_argument("--scan-output", choices=["write", "buffer"], default="write",
+                   help="config 5: the index appended to a bytearray as the scan writes it "
+                        "(cir_scan_v1_write, the reference's v1::scan into a Vec) or returned "
+                        "whole (cir_scan_v1) and copied out")
     p.add_argument("--dry-run-bad-rank", type=int, default=-1,
                    help="--dry-run only: this rank corrupts one digest of its shard (the "
                         "job-wide parity reduction must report FAIL)")
@@ -702,15 +706,25 @@ def run_config5(args, ca, ctx, ctx_init_s=None):
     # footer placement: the library default (host), the GPU chain, or both
     # alternating in one process (--footer ab); every scan is timed per batch
     modes = {"host": ["host"], "gpu": ["gpu"], "ab": ["host", "gpu"]}[args.footer]
+    # the index written into a growing bytearray as the scan emits it
+    # (cir_scan_v1_write, as v1::scan fills the caller's Vec), or returned
+    # whole (cir_scan_v1) and copied into a bytes object after the scan
+    write_out = getattr(args, "scan_output", "write") == "write"
     scans = []
     index = None
     for i in range(max(1, args.steps) * len(modes)):
         mode = modes[i % len(modes)]
         ctx.set_footer_mode(ctx.FOOTER_HOST if mode == "host" else ctx.FOOTER_GPU)
         ctx.scan_timing(True)
-        t0 = time.perf_counter()
-        got = ca.v1.scan(cfg, context=ctx)
-        dt = time.perf_counter() - t0
+        if write_out:  # the reference's call: v1::scan(&cfg, &mut index_buf)
+            t0 = time.perf_counter()
+            got = bytearray()
+            ca.v1.scan(cfg, out=got, context=ctx)
+            dt = time.perf_counter() - t0
+        else:  # the whole index in one library buffer, copied into bytes
+            t0 = time.perf_counter()
+            got = ca.v1.scan(cfg, context=ctx)
+            dt = time.perf_counter() - t0
         ph = ctx.scan_phases()
         summ = scan_batch_summary(ctx.scan_batches(), ph)
         ctx.scan_timing(False)
@@ -721,7 +735,9 @@ def run_config5(args, ca, ctx, ctx_init_s=None):
                       "footer_feeds": int(ph["footer_feeds"]), "batches": summ})
         if index is not None and got != index:
             raise SystemExit("config5: two scans of the same tree differ")
-        index = got
+        if index is None:
+            index = bytes(got)
+        del got
     ctx.set_footer_mode(ctx.FOOTER_HOST)
     times = [sc["seconds"] for sc in scans if sc["footer"] == modes[0]]
     best = min(times)
@@ -767,10 +783,14 @@ def run_config5(args, ca, ctx, ctx_init_s=None):
             "value_first": round(nbytes / times[0] / GIB, 3),
             "context_init_s": round(ctx_init_s, 3) if ctx_init_s is not None else None,
             "config": {"workload": "config5: %d files x 32 MiB in 40 dirs (%.0f GiB) on tmpfs, "
-                                   "cir_scan_v1 (reads -> pinned -> H2D -> hash -> D2H; footer "
+                                   "%s (reads -> pinned -> H2D -> hash -> D2H; footer "
                                    "on %s)" % (nfiles, nbytes / GIB,
+                                               "cir_scan_v1_write into a bytearray as the scan "
+                                               "emits it" if write_out else
+                                               "cir_scan_v1, the index copied out after the scan",
                                                "a host thread" if modes[0] == "host"
                                                else "the GPU chain")},
+            "scan_output": "write" if write_out else "buffer",
             "footer": modes[0], "by_footer_mode": by_mode,
             "hash_type": "sha512/256" if sha else "blake2b/256",
             # the best scan's phases: the footer's busy time (host thread, or

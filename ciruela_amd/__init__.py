@@ -219,6 +219,36 @@ class Context:
                                     ctypes.byref(ln)))
         return _n.take_buffer(out.value, ln.value)
 
+    def scan_into(self, config, out):
+        """cir_scan_v1_write: append the index to `out` (a bytearray) while
+        the scan emits it -- header, then each stretch of the body as files
+        complete, the footer line last -- as v1::scan writes into the
+        caller's Vec (src/client/sync/uploads.rs:55-57).  Returns the number
+        of bytes appended.  An exception raised while appending stops the
+        scan and is re-raised here."""
+        dirs = [os.fsencode(d) for d, _ in config._dirs]
+        pres = [p.encode() for _, p in config._dirs]
+        cd = (ctypes.c_char_p * len(dirs))(*dirs)
+        cp = (ctypes.c_char_p * len(pres))(*pres)
+        failed = []
+
+        def write(_user, data, n):
+            try:
+                out.extend((ctypes.c_char * n).from_address(data))
+                return 0
+            except BaseException as e:  # noqa: BLE001 - re-raised after the call
+                failed.append(e)
+                return 1
+        cb = _n.WRITE_FN(write)
+        ln = ctypes.c_size_t()
+        rc = _n.lib.cir_scan_v1_write(self._h, cd, cp, len(dirs), config._block_size,
+                                      config._hash.code, config._threads, cb, None,
+                                      ctypes.byref(ln))
+        if failed:
+            raise failed[0]
+        _n.check(rc)
+        return ln.value
+
     # ---- footer placement and scan timing (diagnostics) -------------------
     FOOTER_HOST, FOOTER_GPU = 0, 1
     SCAN_BATCH_FIELDS = ("device", "bytes", "blocks", "wait_ms", "read_start_ms", "read_end_ms",
@@ -460,13 +490,17 @@ class ScannerConfig:
 class v1:  # noqa: N801 - mirrors the `dir_signature::v1` module
     @staticmethod
     def scan(config, out=None, context=None):
-        """dir_signature::v1::scan(&cfg, &mut Vec<u8>): index bytes.
+        """dir_signature::v1::scan(&cfg, &mut Vec<u8>).
 
-        Like the reference, appends to `out` (a bytearray) when given."""
-        data = (context or default_context()).scan(config)
+        With `out` (a bytearray), like the reference: the index is appended
+        to it as the scan writes it out (cir_scan_v1_write: no whole-index
+        copy after the scan) and None is returned.  Without, the index bytes
+        are returned (cir_scan_v1)."""
+        ctx = context or default_context()
         if out is not None:
-            out.extend(data)
-        return data
+            ctx.scan_into(config, out)
+            return None
+        return ctx.scan(config)
 
 
 def sha512_256(data):

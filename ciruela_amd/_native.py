@@ -48,6 +48,9 @@ CIR_STAGING_LAZY = (1 << 64) - 1  # cir_init: no staging slots until a host path
 CIR_HASH_BLAKE2B_256 = 1
 CIR_HASH_SHA512_256 = 2
 
+# cir_write_fn: int (*)(void* user, const uint8_t* data, size_t n)
+WRITE_FN = ctypes.CFUNCTYPE(ctypes.c_int, c_vp, c_vp, ctypes.c_size_t)
+
 # name -> (restype, argtypes)
 _SIGS = {
     "cir_init": (ctypes.c_int, [ctypes.POINTER(c_vp), ctypes.c_uint32, ctypes.c_uint64]),
@@ -70,6 +73,10 @@ _SIGS = {
                                    ctypes.POINTER(ctypes.c_char_p), ctypes.c_size_t,
                                    ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32,
                                    ctypes.POINTER(c_vp), c_sizep]),
+    "cir_scan_v1_write": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_char_p),
+                                         ctypes.POINTER(ctypes.c_char_p), ctypes.c_size_t,
+                                         ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32,
+                                         WRITE_FN, c_vp, c_sizep]),
     "cir_index_get_hash": (ctypes.c_int, [c_vp, ctypes.c_size_t, c_vp, c_sizep]),
     "cir_index_rewrite": (ctypes.c_int, [c_vp, c_vp, ctypes.c_size_t, ctypes.POINTER(c_vp),
                                          c_sizep]),

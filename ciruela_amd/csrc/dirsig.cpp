@@ -163,7 +163,21 @@ void Emitter::add_symlink(const std::string& name, const std::string& target) {
   append("\n", 1);
 }
 
+void Emitter::consume(size_t upto) {
+  if (upto <= drop_) return;
+  const size_t n = std::min(upto - drop_, len_);
+  memmove(buf_, buf_ + n, len_ - n);
+  len_ -= n;
+  drop_ += n;
+}
+
+bool Emitter::finish_footer(const uint8_t* footer, size_t footer_len) {
+  append(to_hex(footer, footer_len) + '\n');
+  return !oom_;
+}
+
 uint8_t* Emitter::finish_malloc(const uint8_t* footer, size_t footer_len, size_t* len) {
+  if (drop_) return nullptr;
   append(to_hex(footer, footer_len) + '\n');
   if (oom_) return nullptr;
   uint8_t* out = buf_;

@@ -42,7 +42,10 @@ struct Header {
 // finish_malloc() needs the footer digest of the body (computed by the
 // caller) and appends its hex line.  The index is built in place in one
 // malloc'd buffer (header first), so finishing hands that buffer over
-// without copying the body.
+// without copying the body.  A caller that writes the index out as it goes
+// (cir_scan_v1_write) drops what it has written with consume(), so the
+// buffer holds only the unwritten tail; offsets stay absolute (bytes since
+// the start of the index, or of the body) across a consume().
 class Emitter {
  public:
   explicit Emitter(const Header& h);
@@ -55,14 +58,26 @@ class Emitter {
   void add_file(const std::string& name, bool exe, uint64_t size, const uint8_t* hashes,
                 size_t nhash);
   void add_symlink(const std::string& name, const std::string& target);
-  // Bytes the footer hashes: everything after the header line.  The pointer
-  // moves when the buffer grows; an offset into the body stays valid.
-  const char* body_data() const { return (const char*)buf_ + hlen_; }
-  size_t body_size() const { return len_ - hlen_; }
+  // Bytes the footer hashes: everything after the header line.  A pointer
+  // moves when the buffer grows or is consumed; an offset into the body
+  // stays valid.  body_at(off) needs off at or past what consume() dropped.
+  const char* body_at(size_t off) const { return (const char*)buf_ + hlen_ + off - drop_; }
+  const char* body_data() const { return body_at(0); }  // nothing of the body consumed
+  size_t body_size() const { return drop_ + len_ - hlen_; }
+  // the whole index so far: bytes [0, index_size()), held from consumed() on
+  size_t index_size() const { return drop_ + len_; }
+  size_t consumed() const { return drop_; }
+  size_t header_size() const { return hlen_; }
+  const uint8_t* index_at(size_t off) const { return buf_ + off - drop_; }
+  // drop the index bytes before offset `upto` (consumed() <= upto <= index_size())
+  void consume(size_t upto);
   // header + body + hex footer + newline in one malloc'd buffer (free()),
   // which the emitter gives up; null if out of memory (or after an append
-  // failed to allocate).
+  // failed to allocate), or if anything was consumed.
   uint8_t* finish_malloc(const uint8_t* footer, size_t footer_len, size_t* len);
+  // append the hex footer line only (the streaming form); false if out of memory
+  bool finish_footer(const uint8_t* footer, size_t footer_len);
+  bool failed() const { return oom_; }
   const std::string& header_line() const { return header_; }
 
  private:
@@ -72,6 +87,7 @@ class Emitter {
   std::string header_;
   uint8_t* buf_ = nullptr;
   size_t len_ = 0, cap_ = 0, hlen_ = 0;
+  size_t drop_ = 0;  // index bytes consumed before buf_[0]
   bool oom_ = false;
 };
 

@@ -499,7 +499,7 @@ struct FooterChain {
                   cap / 1048576.0, now_ms() - ta);
       }
       if (piece) {
-        memcpy(d.chain_h[k], em.body_data() + fed, piece);
+        memcpy(d.chain_h[k], em.body_at(fed), piece);
         CIR_HIP(hipMemcpyAsync(d.chain_d[k], d.chain_h[k], piece, hipMemcpyHostToDevice, d.chain));
       }
       hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -559,7 +559,7 @@ class HostFooter {
     if (n == 0 || n < min_feed) return;
     {
       std::lock_guard<std::mutex> lk(mu_);
-      q_.emplace_back(em.body_data() + fed_, n);
+      q_.emplace_back(em.body_at(fed_), n);
     }
     cv_.notify_one();
     fed_ += n;
@@ -660,10 +660,23 @@ using namespace cir;
 
 extern "C" {
 
-int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefixes, size_t ndirs,
-                uint64_t block_size, int hash_type, uint32_t threads, uint8_t** index_out,
-                size_t* len_out) {
-  if (!ctx || !index_out || !len_out || (ndirs && !dirs)) return fail(CIR_EINVAL, "null pointer");
+// cir_scan_v1 (the index in one malloc'd buffer) and cir_scan_v1_write (the
+// index written out to `write` as it is emitted: header first, then each
+// stretch of the body after every batch that completes files, the footer
+// line last; the emitter keeps only the unwritten tail).
+namespace {
+struct IndexSink {
+  cir_write_fn write;
+  void* user;
+};
+}  // namespace
+
+static int scan_impl(cir_ctx* ctx, const char* const* dirs, const char* const* prefixes,
+                     size_t ndirs, uint64_t block_size, int hash_type, uint32_t threads,
+                     const IndexSink* sink, uint8_t** index_out, size_t* len_out) {
+  if (!ctx || (!sink && (!index_out || !len_out)) || (ndirs && !dirs))
+    return fail(CIR_EINVAL, "null pointer");
+  if (sink && !sink->write) return fail(CIR_EINVAL, "null index writer");
   if (block_size == 0 || block_size > 0xffffffffull)
     return fail(CIR_EINVAL, "block_size must be in 1 .. 2^32-1");
   dirsig::Header hdr;
@@ -709,6 +722,8 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
       if (it.kind == dirsig::EntryKind::kFile)
         est += 65 * ((files[it.file].size + block_size - 1) / block_size);
     }
+    // (streamed out: the buffer holds one batch's text at a time)
+    if (sink) est = std::min<size_t>(est, (size_t)4 << 20);
     if (!em.reserve_body(est + est / 64)) return fail(CIR_ENOMEM, "index buffer");
   }
   Device& dv = *ctx->devs[0];
@@ -723,6 +738,25 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
   if (rc) return rc;
   DigestBuf digests;
   size_t plan_pos = 0;
+  size_t sunk = 0;  // index bytes handed to the sink
+  size_t writes = 0;
+  // hand the new index bytes to the sink, then drop from the emitter what
+  // both the sink and the footer are done with (the footer feeds hold body
+  // offsets: a GPU-chain feed keeps a partial line back)
+  auto flush = [&]() -> int {
+    if (!sink) return CIR_OK;
+    if (em.failed()) return fail(CIR_ENOMEM, "index buffer");
+    const size_t end = em.index_size();
+    if (end > sunk) {
+      if (sink->write(sink->user, em.index_at(sunk), end - sunk) != 0)
+        return fail(CIR_EIO, "index writer failed");
+      sunk = end;
+      ++writes;
+    }
+    const size_t footer_fed = hfoot ? hfoot->fed() : gpu_chain ? chain.fed : 0;
+    em.consume(std::min(sunk, em.header_size() + footer_fed));
+    return CIR_OK;
+  };
   // emit every plan item whose file blocks are all hashed (files complete in
   // plan order), then feed the finished stretch of the body to the footer
   auto emit_ready = [&](uint64_t done_blk) -> int {
@@ -740,7 +774,8 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
       }
     }
     if (hfoot) hfoot->advance(em, (size_t)256 << 10);
-    return gpu_chain ? chain.advance(em, (size_t)256 << 10) : (int)CIR_OK;
+    const int rc = gpu_chain ? chain.advance(em, (size_t)256 << 10) : (int)CIR_OK;
+    return rc ? rc : flush();
   };
   const double t1 = now_ms();
   rc = hash_files(ctx, files, block_size, threads, hash_type, digests, emit_ready,
@@ -763,13 +798,24 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
     const uint64_t off = 0;
     const uint32_t blen = (uint32_t)em.body_size();
     static const uint8_t empty = 0;
+    // (nothing of the body was consumed: no footer feed held it)
     rc = cir_hash_blocks_ht(ctx, hash_type,
-                            blen ? (const uint8_t*)em.body_data() : &empty, &off, &blen, 1, footer);
+                            blen ? (const uint8_t*)em.body_at(0) : &empty, &off, &blen, 1, footer);
   }
   if (rc) return rc;
   const double t4 = now_ms();
-  *index_out = em.finish_malloc(footer, 32, len_out);
-  if (!*index_out) return fail(CIR_ENOMEM, "malloc");
+  size_t total = 0;
+  if (sink) {
+    if (!em.finish_footer(footer, 32)) return fail(CIR_ENOMEM, "index buffer");
+    rc = flush();
+    if (rc) return rc;
+    total = sunk;
+    if (len_out) *len_out = total;
+  } else {
+    *index_out = em.finish_malloc(footer, 32, &total);
+    if (!*index_out) return fail(CIR_ENOMEM, "malloc");
+    *len_out = total;
+  }
   const double t5 = now_ms();
   if (stats) {
     std::lock_guard<std::mutex> sl(ctx->stats.mu);
@@ -781,16 +827,32 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
                          hfoot ? hfoot->busy_ms() : gpu_chain ? chain.busy_ms() : 0.0,
                          (double)(hfoot ? CIR_FOOTER_HOST : CIR_FOOTER_GPU),
                          (double)(ctx->stats.batches.size() - rows0),
-                         (double)*len_out,
+                         (double)total,
                          (double)(hfoot ? hfoot->feeds() : chain.feeds)};
     ++ctx->stats.scans;
   }
   if (trace_on())
     fprintf(stderr,
             "cir_scan phases: walk %.1f ms, hash loop %.1f ms, last emit %.1f ms, footer %.1f ms, "
-            "output %.1f ms; %zu files, index %.1f MiB\n",
-            t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4, files.size(), *len_out / 1048576.0);
+            "output %.1f ms; %zu files, index %.1f MiB%s\n",
+            t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4, files.size(), total / 1048576.0,
+            sink ? (", written in " + std::to_string(writes) + " pieces").c_str() : "");
   return CIR_OK;
+}
+
+int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefixes, size_t ndirs,
+                uint64_t block_size, int hash_type, uint32_t threads, uint8_t** index_out,
+                size_t* len_out) {
+  return scan_impl(ctx, dirs, prefixes, ndirs, block_size, hash_type, threads, nullptr, index_out,
+                   len_out);
+}
+
+int cir_scan_v1_write(cir_ctx* ctx, const char* const* dirs, const char* const* prefixes,
+                      size_t ndirs, uint64_t block_size, int hash_type, uint32_t threads,
+                      cir_write_fn write, void* user, size_t* len_out) {
+  const IndexSink sink{write, user};
+  return scan_impl(ctx, dirs, prefixes, ndirs, block_size, hash_type, threads, &sink, nullptr,
+                   len_out);
 }
 
 // RawIndex::into_mut + MutableIndex::to_raw_data: parse, rebuild the tree and

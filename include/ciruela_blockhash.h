@@ -205,6 +205,21 @@ int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefix
                 uint64_t block_size, int hash_type, uint32_t threads, uint8_t** index_out,
                 size_t* len_out);
 
+/* The same scan writing the index out as it goes, as v1::scan writes into
+ * the caller's `&mut Vec<u8>` / io::Write (src/client/sync/uploads.rs:55-57):
+ * write(user, data, n) receives the index bytes in order -- the header line
+ * first, then each stretch of the body as the batches complete files, the
+ * footer line last -- from library threads, one call at a time.  The
+ * library keeps only the unwritten tail (no whole-index buffer, no copy
+ * after the scan).  A non-zero return from write stops the scan with
+ * CIR_EIO (the reference's io::Error from the writer); on any error the
+ * writer may have received part of an index.  *len_out (may be NULL) = the
+ * bytes written. */
+typedef int (*cir_write_fn)(void* user, const uint8_t* data, size_t n);
+int cir_scan_v1_write(cir_ctx* ctx, const char* const* dirs, const char* const* prefixes,
+                      size_t ndirs, uint64_t block_size, int hash_type, uint32_t threads,
+                      cir_write_fn write, void* user, size_t* len_out);
+
 /* dir_signature::get_hash via InMemoryIndexes::register_index
  * (src/index.rs:98-105): the image id printed on the index's last line.
  * id_out must hold 64 bytes; *id_len = decoded length (32 for v1 hashes). */

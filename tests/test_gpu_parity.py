@@ -771,6 +771,76 @@ def test_scan_long_index_footer(gpu, small_ctx, tmp_path, mode, hash_name):
     assert ph["index_bytes"] == len(got)
 
 
+class CountingBuffer(bytearray):
+    """A bytearray that counts the appends cir_scan_v1_write makes into it."""
+    pieces = 0
+
+    def extend(self, data):
+        self.pieces += 1
+        super().extend(data)
+
+
+@pytest.mark.parametrize("hash_name", ["blake2b/256", "sha512/256"])
+@pytest.mark.parametrize("mode", ["host", "gpu"])
+def test_scan_written_as_it_goes(gpu, small_ctx, tmp_path, mode, hash_name):
+    """cir_scan_v1_write (v1::scan into the caller's Vec, src/client/sync/
+    uploads.rs:55-57): a several-MiB index arrives in many pieces while the
+    batches run -- header first, the footer line last -- and equals the
+    oracle's index byte for byte with either footer placement (the library
+    keeps only the unwritten tail; a sha512/256 footer in GPU mode keeps the
+    whole body for its one-lane hash at the end)."""
+    rng = random.Random(6)
+    for k in range(6):
+        (tmp_path / ("f%d.bin" % k)).write_bytes(rng.randbytes(rng.randrange(1 << 20, 3 << 20)))
+    ht = gpu.HashType.sha512_256() if hash_name == "sha512/256" else gpu.HashType.blake2b_256()
+    cfg = gpu.ScannerConfig.new().block_size(128).hash(ht).add_dir(str(tmp_path), "/")
+    small_ctx.set_footer_mode(small_ctx.FOOTER_HOST if mode == "host" else small_ctx.FOOTER_GPU)
+    small_ctx.scan_timing(True)
+    try:
+        out = CountingBuffer(b"keep:")  # appended to, as the reference's Vec
+        assert gpu.v1.scan(cfg, out=out, context=small_ctx) is None
+        ph = small_ctx.scan_phases()
+    finally:
+        small_ctx.scan_timing(False)
+        small_ctx.set_footer_mode(small_ctx.FOOTER_HOST)
+    want = dirsig_oracle.scan(str(tmp_path), 128, hash_name)
+    assert bytes(out) == b"keep:" + want
+    assert out.pieces >= 4, out.pieces
+    assert ph["index_bytes"] == len(want)
+
+
+def test_scan_writer_failure_is_an_io_error(gpu, small_ctx, tmp_path):
+    """A writer that fails (the reference's io::Error from the Vec/Write)
+    stops the scan: the exception comes back to the caller, the C status is
+    CIR_EIO, and the context scans normally afterwards."""
+    n = gpu._n
+    rng = random.Random(8)
+    for k in range(4):
+        (tmp_path / ("f%d.bin" % k)).write_bytes(rng.randbytes(1 << 20))
+    cfg = gpu.ScannerConfig.new().block_size(1024).add_dir(str(tmp_path), "/")
+
+    class Full(bytearray):
+        def extend(self, data):
+            if len(self) > 0:
+                raise OSError(28, "No space left on device")
+            super().extend(data)
+    with pytest.raises(OSError):
+        gpu.v1.scan(cfg, out=Full(), context=small_ctx)
+    calls = []
+
+    @n.WRITE_FN
+    def refuse(_user, _data, _n):
+        calls.append(1)
+        return 7
+    dirs = (ctypes.c_char_p * 1)(os.fsencode(str(tmp_path)))
+    pres = (ctypes.c_char_p * 1)(b"/")
+    rc = n.lib.cir_scan_v1_write(small_ctx.handle, dirs, pres, 1, 1024, 1, 0, refuse, None, None)
+    assert rc == n.CIR_EIO and calls == [1]
+    out = bytearray()
+    gpu.v1.scan(cfg, out=out, context=small_ctx)
+    assert bytes(out) == dirsig_oracle.scan(str(tmp_path), 1024)
+
+
 def test_scan_timing_rows(gpu, tmp_path):
     """cir_debug_scan_timing: one row per staged batch (bytes add up to the
     tree's, block counts to its blocks), each batch's events in order (reads,
@@ -1572,8 +1642,9 @@ def random_tree(root, rng, bs):
 def scan_case(gpu, seed, tmp_path, monkeypatch):
     """One randomized end-to-end scan against the scan oracle, over the
     scan's knobs: block size, hash type, reader threads, staging size, the
-    staging copy mode, the footer's placement and a split over 1-3 device
-    states (CIR_DEBUG_SPLIT on the one GPU)."""
+    staging copy mode, the footer's placement, a split over 1-3 device
+    states (CIR_DEBUG_SPLIT on the one GPU) with stripes of 1-5 blocks or the
+    default, and the index returned whole or written out as it goes."""
     rng = random.Random(seed)
     bs = rng.choice([128, 1000, 4096, 32768, 65536 + 3])
     root = tmp_path / ("t%d" % seed)
@@ -1595,7 +1666,12 @@ def scan_case(gpu, seed, tmp_path, monkeypatch):
     ht = gpu.HashType.sha512_256() if hash_name == "sha512/256" else gpu.HashType.blake2b_256()
     cfg = gpu.ScannerConfig.new().block_size(bs).threads(rng.choice([0, 1, 3, 4])).hash(ht)
     cfg.add_dir(str(root), "/")
-    got = gpu.v1.scan(cfg, context=ctx)
+    if rng.random() < 0.5:  # written out as it goes (cir_scan_v1_write)
+        out = bytearray()
+        gpu.v1.scan(cfg, out=out, context=ctx)
+        got = bytes(out)
+    else:
+        got = gpu.v1.scan(cfg, context=ctx)
     monkeypatch.delenv("CIR_DEBUG_STRIPE_BLOCKS", raising=False)
     want = dirsig_oracle.scan(str(root), bs, hash_name)
     assert got == want, (seed, bs, hash_name, split)
