@@ -658,8 +658,6 @@ static void emit_tree(dirsig::Emitter& em, const std::string& path, const Tree& 
 
 using namespace cir;
 
-extern "C" {
-
 // cir_scan_v1 (the index in one malloc'd buffer) and cir_scan_v1_write (the
 // index written out to `write` as it is emitted: header first, then each
 // stretch of the body after every batch that completes files, the footer
@@ -839,6 +837,8 @@ static int scan_impl(cir_ctx* ctx, const char* const* dirs, const char* const* p
             sink ? (", written in " + std::to_string(writes) + " pieces").c_str() : "");
   return CIR_OK;
 }
+
+extern "C" {
 
 int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefixes, size_t ndirs,
                 uint64_t block_size, int hash_type, uint32_t threads, uint8_t** index_out,
