@@ -91,3 +91,27 @@ def test_cpu_indexer_matches_scan_oracle(tmp_path):
     # and with dir-signature's other hash type (bench.py config 5 --hash sha512)
     want = dirsig_oracle.scan(str(tmp_path), 4096, "sha512/256")
     assert cpu_indexer.index(str(tmp_path), 4096, 3, hash_name="sha512/256") == want
+
+
+def test_emitter_streaming_sanitized(tmp_path):
+    """The emitter's streaming form (Emitter::consume, as cir_scan_v1_write
+    drives it) under AddressSanitizer + UBSan, g++ on dirsig.cpp alone: random
+    entries written out in random pieces, with the written and footer-fed
+    prefix dropped, give exactly the whole index, and the footer feed exactly
+    its body (tools/emitter_stream_fuzz.cpp)."""
+    import shutil
+    import subprocess
+    if shutil.which("g++") is None:
+        import pytest
+        pytest.skip("needs g++")
+    from conftest import ROOT
+    csrc = os.path.join(ROOT, "ciruela_amd", "csrc")
+    exe = str(tmp_path / "emitter_stream_fuzz")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
+                    "-fno-sanitize-recover=all", "-I" + csrc,
+                    os.path.join(ROOT, "tools", "emitter_stream_fuzz.cpp"),
+                    os.path.join(csrc, "dirsig.cpp"), "-o", exe], check=True)
+    for seed in (1, 2):
+        p = subprocess.run([exe, "80", str(seed)], capture_output=True, timeout=300)
+        assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
+        assert b"no sanitizer report" in p.stdout
