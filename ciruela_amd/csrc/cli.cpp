@@ -162,8 +162,12 @@ int main(int argc, char** argv) {
     const int n = cir_device_count();
     fprintf(stderr, "ciruela-index: HIP runtime start %.1f ms (%d devices)\n", ms_since(t0), n);
   }
+  // an input below one staging slot (256 MiB) is one batch on one GPU: open
+  // only the first visible device instead of every GPU of the node (each
+  // costs its device context, streams and pinned staging at start-up)
+  const uint32_t mask = staging ? 1u : 0u;
   const auto t_init = std::chrono::steady_clock::now();
-  int rc = cir_init(&ctx, 0, staging);
+  int rc = cir_init(&ctx, mask, staging);
   if (rc) return die(rc, "cir_init");
   if (trace) fprintf(stderr, "ciruela-index: cir_init %.1f ms\n", ms_since(t_init));
   if (cmd == "hash") {
