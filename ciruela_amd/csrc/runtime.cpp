@@ -140,6 +140,11 @@ bool stage_copy_nt() {  // read per API call / batch: tests switch it within one
   return !(v && strcmp(v, "direct") == 0);
 }
 
+bool scan_ramp() {  // read per call
+  const char* v = std::getenv("CIR_STAGE_RAMP");
+  return !(v && strcmp(v, "0") == 0);
+}
+
 // 16-B aligned non-temporal stores; the unaligned head and the tail with
 // plain stores; sfence so the bytes are globally visible before the caller
 // hands the slot to the copy engine.
@@ -615,6 +620,9 @@ static int run_file_dev(cir_ctx* ctx, Device& d, const Reader& rd, uint64_t bs,
   uint64_t chunk = ctx->staging / bs * bs;
   if (chunk == 0) chunk = bs;
   const uint64_t chunk_blk = chunk / bs;
+  // the first batches ramp up (1/8, 1/4, 1/2 of a slot, then whole slots),
+  // as the scan's do: the first upload starts after a short fill
+  uint64_t fill = scan_ramp() ? std::max<uint64_t>(bs, chunk / 8 / bs * bs) : chunk;
   uint64_t total = 0;
   bool eof = false;
   size_t pending_at[2] = {0, 0}, pending_n[2] = {0, 0};
@@ -633,8 +641,10 @@ static int run_file_dev(cir_ctx* ctx, Device& d, const Reader& rd, uint64_t bs,
       int rc = d.ensure_slot(s, chunk, chunk_blk);
       if (rc) return rc;
       uint64_t got = 0;
-      while (got < chunk) {
-        const int64_t r = rd(s.h_data + got, chunk - got);
+      const uint64_t want = fill;
+      fill = std::min(chunk, fill * 2);
+      while (got < want) {
+        const int64_t r = rd(s.h_data + got, want - got);
         if (r < 0) return fail(CIR_EIO, std::string("read: ") + strerror((int)-r));
         if (r == 0) {
           eof = true;

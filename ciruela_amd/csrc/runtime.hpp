@@ -96,6 +96,9 @@ unsigned host_copy_threads(size_t ndev);
 // upload at 4.8-6.2 ms while the readers run; nt 47.8-48.6 GiB/s, every
 // upload 4.75 ms (the link's rate) and the reads faster too.
 bool stage_copy_nt();
+// CIR_STAGE_RAMP=0: the staged host paths (scan, hash_file, hash_memory)
+// start with whole-slot batches instead of ramping up from 1/8 of a slot.
+bool scan_ramp();
 // n bytes into a staging slot from memory / from fd at off (pread
 // semantics: the count read, 0 at EOF, -1 with errno), with streaming
 // stores when nt (the caller reads stage_copy_nt() once per call or batch).

@@ -222,6 +222,10 @@ static int hash_range(cir_ctx* ctx, Device& d, size_t di, const std::vector<Scan
   std::vector<std::array<double, kScanBatchFields>> rows;
   const uint64_t cap = std::max<uint64_t>(ctx->staging, bs + 16);
   const uint64_t cap_blk = std::max<uint64_t>(cap / 512, 4096);
+  // the first batches ramp up (1/8, 1/4, 1/2 of a slot, then whole slots):
+  // the first upload starts after a short read instead of a whole slot's,
+  // and each read still finishes within the previous upload
+  uint64_t fill = scan_ramp() ? std::max<uint64_t>(bs + 16, cap >> 3) : cap;
   size_t ri = 0;  // the range being packed
   uint64_t b0 = 0, b1 = 0;
   size_t fi = 0;
@@ -305,13 +309,13 @@ static int hash_range(cir_ctx* ctx, Device& d, size_t di, const std::vector<Scan
         const uint64_t left_blk = std::min<uint64_t>((f.size + bs - 1) / bs - fblk,
                                                      b1 - (f.first_blk + fblk));
         pos = (pos + 15) & ~15ull;
-        if (pos + std::min<uint64_t>(bs, f.size - fblk * bs) > cap) break;
+        if (pos + std::min<uint64_t>(bs, f.size - fblk * bs) > fill) break;
         // as many whole blocks of this file as fit
         uint64_t take = std::min<uint64_t>(left_blk, cap_blk - n);
-        take = std::min<uint64_t>(take, std::max<uint64_t>((cap - pos) / bs, 1));
+        take = std::min<uint64_t>(take, std::max<uint64_t>((fill - pos) / bs, 1));
         const uint64_t off0 = fblk * bs;
         const uint64_t bytes = std::min<uint64_t>(take * bs, f.size - off0);
-        if (pos + bytes > cap) break;
+        if (pos + bytes > fill) break;
         for (uint64_t j = 0; j < take; ++j) {
           s.h_off[n + j] = pos + j * bs;
           s.h_len[n + j] = (uint32_t)std::min<uint64_t>(bs, f.size - off0 - j * bs);
@@ -323,6 +327,7 @@ static int hash_range(cir_ctx* ctx, Device& d, size_t di, const std::vector<Scan
         n += take;
         fblk += take;
       }
+      fill = std::min(cap, fill * 2);
       const double t_read0 = clock ? now_ms() : 0;
       rc = run_reads(jobs, files, threads);
       if (rc) return rc;

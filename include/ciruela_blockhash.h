@@ -26,6 +26,10 @@
  *       CIR_STAGE_COPY=direct  host threads fill the pinned staging slots with
  *                              plain pread()/memcpy() instead of streaming
  *                              (non-temporal) stores;
+ *       CIR_STAGE_RAMP=0       staged host paths start with whole-slot batches
+ *                              (default: the first three batches ramp up from
+ *                              1/8 of a slot, so the first upload starts
+ *                              sooner);
  *       CIR_FOOTER=gpu         cir_init's contexts start with CIR_FOOTER_GPU;
  *       CIR_TRACE=1            per-batch timings on stderr;
  *       CIR_DEBUG_SPLIT=k      (tests) every opened GPU appears k times.
