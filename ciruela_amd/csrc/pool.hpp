@@ -1,0 +1,100 @@
+// The host worker pool behind parallel_run (runtime.hpp): the staged host
+// paths' reader and copy threads (scan.cpp run_reads, runtime.cpp
+// parallel_pieces / parallel_items) persist across batches instead of being
+// created and joined per batch.  Header-only so that a CPU stress test can
+// build it alone under ThreadSanitizer (tools/pool_stress.cpp).
+#pragma once
+#include <algorithm>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace cir {
+
+// A call queues n-1 tickets for its job and runs the job itself; a worker
+// takes a ticket, runs the job and counts it off.  The job pulls its items
+// from shared state and returns when none are left, so once the caller's own
+// run returns, tickets nobody has started are dropped rather than waited
+// for: a busy pool delays a call by at most the tickets already running.
+class WorkerPool {
+ public:
+  static constexpr size_t kMaxWorkers = 256;
+
+  WorkerPool() = default;
+  WorkerPool(const WorkerPool&) = delete;
+  WorkerPool& operator=(const WorkerPool&) = delete;
+  // (the process-wide pool is never destroyed; a pool that is waits for its
+  // workers, which must be idle: no run() in progress)
+  ~WorkerPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (std::thread& t : th_) t.join();
+  }
+
+  void run(unsigned n, const std::function<void()>& fn) {
+    if (n <= 1) {
+      fn();
+      return;
+    }
+    Job job;
+    job.fn = &fn;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      while (th_.size() < std::min<size_t>(n - 1, kMaxWorkers)) th_.emplace_back([this] { loop(); });
+      for (unsigned i = 0; i + 1 < n; ++i) q_.push_back(&job);
+      job.pending = n - 1;
+    }
+    cv_.notify_all();
+    fn();
+    std::unique_lock<std::mutex> lk(mu_);
+    for (auto it = q_.begin(); it != q_.end();) {
+      if (*it == &job) {
+        it = q_.erase(it);
+        --job.pending;
+      } else {
+        ++it;
+      }
+    }
+    job.done.wait(lk, [&] { return job.pending == 0; });
+  }
+
+  size_t workers() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return th_.size();
+  }
+
+ private:
+  struct Job {
+    const std::function<void()>* fn = nullptr;
+    unsigned pending = 0;  // tickets queued or running (under mu_)
+    std::condition_variable done;
+  };
+
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+      if (q_.empty()) return;  // stopping
+      Job* j = q_.front();
+      q_.pop_front();
+      lk.unlock();
+      (*j->fn)();
+      lk.lock();
+      if (--j->pending == 0) j->done.notify_all();
+    }
+  }
+
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<Job*> q_;
+  std::vector<std::thread> th_;
+  bool stop_ = false;
+};
+
+}  // namespace cir

@@ -4,6 +4,8 @@
 // each entry point replaces.
 #include "runtime.hpp"
 
+#include "pool.hpp"
+
 #include <emmintrin.h>
 #include <errno.h>
 #include <sched.h>
@@ -15,8 +17,8 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
-#include <cstdlib>
 #include <condition_variable>
+#include <cstdlib>
 #include <deque>
 #include <thread>
 #include <unordered_map>
@@ -140,6 +142,13 @@ bool stage_copy_nt() {  // read per API call / batch: tests switch it within one
   return !(v && strcmp(v, "direct") == 0);
 }
 
+static WorkerPool& pool() {  // never destroyed: a context's threads may still use it at exit
+  static WorkerPool* p = new WorkerPool;
+  return *p;
+}
+
+void parallel_run(unsigned n, const std::function<void()>& work) { pool().run(n, work); }
+
 bool scan_ramp() {  // read per call
   const char* v = std::getenv("CIR_STAGE_RAMP");
   return !(v && strcmp(v, "0") == 0);
@@ -175,28 +184,15 @@ void copy_staged(uint8_t* dst, const uint8_t* src, size_t n, bool nt) {
     memcpy(dst, src, n);
 }
 
-// Bounce buffers for pread_staged, reused across calls and threads (the
-// reader threads are created per batch).
+// One bounce buffer per reading thread (the pool's workers persist, so each
+// keeps its buffer warm in its core's L2).
 constexpr size_t kBounce = 512u << 10;
-static struct BouncePool {
-  std::mutex mu;
-  std::vector<uint8_t*> free;
-  ~BouncePool() {
-    for (uint8_t* p : free) delete[] p;
-  }
-} g_bounce;
 
 ssize_t pread_staged(int fd, uint8_t* dst, size_t n, off_t off, bool nt) {
   if (!nt || n < 4096) return ::pread(fd, dst, n, off);
-  uint8_t* b = nullptr;
-  {
-    std::lock_guard<std::mutex> lk(g_bounce.mu);
-    if (!g_bounce.free.empty()) {
-      b = g_bounce.free.back();
-      g_bounce.free.pop_back();
-    }
-  }
-  if (!b) b = new uint8_t[kBounce];
+  thread_local std::unique_ptr<uint8_t[]> tl_bounce;
+  if (!tl_bounce) tl_bounce.reset(new uint8_t[kBounce]);
+  uint8_t* b = tl_bounce.get();
   size_t got = 0;
   ssize_t last = 0;
   while (got < n) {
@@ -208,12 +204,6 @@ ssize_t pread_staged(int fd, uint8_t* dst, size_t n, off_t off, bool nt) {
     got += (size_t)last;
     if ((size_t)last < want) break;  // a short read (EOF): the caller decides
   }
-  const int e = errno;
-  {
-    std::lock_guard<std::mutex> lk(g_bounce.mu);
-    g_bounce.free.push_back(b);
-  }
-  errno = e;
   if (got > 0) return (ssize_t)got;
   return last;  // 0 at EOF, -1 with errno
 }
@@ -471,13 +461,7 @@ static int64_t parallel_pieces(uint64_t n, const std::function<int64_t(uint64_t,
       }
     }
   };
-  if (nt <= 1) {
-    work();
-  } else {
-    std::vector<std::thread> th;
-    for (unsigned i = 0; i < nt; ++i) th.emplace_back(work);
-    for (auto& t : th) t.join();
-  }
+  parallel_run(std::max(1u, nt), work);
   return err.load();
 }
 
@@ -494,9 +478,7 @@ static void parallel_items(size_t n, uint64_t bytes, const std::function<void(si
   auto work = [&] {
     for (size_t i0; (i0 = next.fetch_add(grain)) < n;) fn(i0, std::min(n, i0 + grain));
   };
-  std::vector<std::thread> th;
-  for (unsigned i = 0; i < nt; ++i) th.emplace_back(work);
-  for (auto& t : th) t.join();
+  parallel_run(nt, work);
 }
 
 

@@ -96,6 +96,13 @@ unsigned host_copy_threads(size_t ndev);
 // upload at 4.8-6.2 ms while the readers run; nt 47.8-48.6 GiB/s, every
 // upload 4.75 ms (the link's rate) and the reads faster too.
 bool stage_copy_nt();
+// Run `work` on n threads at once -- the caller and n-1 threads of a
+// process-wide pool that persists across calls (created on first use, grown
+// on demand) -- and return when every copy has returned.  `work` must pull
+// its items from shared state (an atomic index) and return once none are
+// left: copies still queued when the caller's own copy returns are dropped.
+// Round 4: the host paths created their reader / copy threads per batch.
+void parallel_run(unsigned n, const std::function<void()>& work);
 // CIR_STAGE_RAMP=0: the staged host paths (scan, hash_file, hash_memory)
 // start with whole-slot batches instead of ramping up from 1/8 of a slot.
 bool scan_ramp();

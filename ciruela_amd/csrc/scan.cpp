@@ -164,14 +164,7 @@ static int run_reads(const std::vector<ReadJob>& jobs, const std::vector<ScanFil
       }
     }
   };
-  const unsigned n = std::max(1u, std::min<unsigned>(threads, (unsigned)jobs.size()));
-  if (n == 1) {
-    worker();
-  } else {
-    std::vector<std::thread> th;
-    for (unsigned i = 0; i < n; ++i) th.emplace_back(worker);
-    for (auto& t : th) t.join();
-  }
+  parallel_run(std::max(1u, std::min<unsigned>(threads, (unsigned)jobs.size())), worker);
   if (rc.load()) return fail(rc.load(), err);
   return CIR_OK;
 }
