@@ -46,9 +46,12 @@ class WorkerPool {
     job.fn = &fn;
     {
       std::lock_guard<std::mutex> lk(mu_);
-      while (th_.size() < std::min<size_t>(n - 1, kMaxWorkers)) th_.emplace_back([this] { loop(); });
       for (unsigned i = 0; i + 1 < n; ++i) q_.push_back(&job);
       job.pending = n - 1;
+      // a worker for every ticket queued or running, concurrent callers
+      // included (several devices' readers at once)
+      const size_t want = std::min<size_t>(busy_ + q_.size(), kMaxWorkers);
+      while (th_.size() < want) th_.emplace_back([this] { loop(); });
     }
     cv_.notify_all();
     fn();
@@ -83,9 +86,11 @@ class WorkerPool {
       if (q_.empty()) return;  // stopping
       Job* j = q_.front();
       q_.pop_front();
+      ++busy_;
       lk.unlock();
       (*j->fn)();
       lk.lock();
+      --busy_;
       if (--j->pending == 0) j->done.notify_all();
     }
   }
@@ -94,6 +99,7 @@ class WorkerPool {
   std::condition_variable cv_;
   std::deque<Job*> q_;
   std::vector<std::thread> th_;
+  size_t busy_ = 0;  // workers running a ticket
   bool stop_ = false;
 };
 

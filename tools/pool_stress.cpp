@@ -8,6 +8,7 @@
 #include <stdlib.h>
 
 #include <atomic>
+#include <chrono>
 #include <random>
 #include <thread>
 #include <vector>
@@ -42,6 +43,32 @@ int main(int argc, char** argv) {
       }
     });
   for (auto& t : th) t.join();
+  // concurrent callers get workers of their own: CALLERS calls of width 12
+  // at once grow the pool to about CALLERS x 11
+  {
+    std::vector<std::thread> wide;
+    std::atomic<int> inside{0}, peak{0};
+    for (int c = 0; c < callers; ++c)
+      wide.emplace_back([&] {
+        std::atomic<int> next{0};
+        pool.run(12, [&] {
+          for (int i; (i = next.fetch_add(1)) < 12;) {
+            const int now = inside.fetch_add(1) + 1;
+            int p = peak.load();
+            while (now > p && !peak.compare_exchange_weak(p, now)) {
+            }
+            std::this_thread::sleep_for(std::chrono::milliseconds(20));
+            inside.fetch_sub(1);
+          }
+        });
+      });
+    for (auto& t : wide) t.join();
+    if (peak.load() < callers * 6) {
+      printf("FAIL: %d concurrent calls of width 12 peaked at %d items in flight\n", callers,
+             peak.load());
+      return 1;
+    }
+  }
   if (bad.load() || pool.workers() > cir::WorkerPool::kMaxWorkers) {
     printf("FAIL: %d items not processed exactly once\n", bad.load());
     return 1;
