@@ -13,7 +13,7 @@ for f in kernels order; do
   /opt/rocm/bin/hipcc $flags --offload-arch=gfx950 -mcode-object-version=5 "$@" \
     -c ciruela_amd/csrc/$f.hip -o "$obj/$f.o" &
 done
-for f in runtime dirsig scan registry; do
+for f in runtime dirsig scan registry blake2b_host sha512_host; do
   /opt/rocm/bin/hipcc $flags -x c++ -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include "$@" \
     -c ciruela_amd/csrc/$f.cpp -o "$obj/$f.o" &
 done
