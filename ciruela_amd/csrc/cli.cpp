@@ -232,6 +232,22 @@ int main(int argc, char** argv) {
     usage();
     return 2;
   }
+  // A one-shot process: every result is written and every GPU call has
+  // completed (the scan synchronises before it returns), so the context's
+  // teardown -- freeing the pinned staging, streams and device buffers one by
+  // one, ~17 ms of a ~0.2 s run (profiles/r04/cli_startup.log) -- is left to
+  // process exit, as the error paths above already do.  CIR_CLI_TEARDOWN=1
+  // destroys the context first (leak checks).
+  const char* td = getenv("CIR_CLI_TEARDOWN");
+  if (!(td && *td && strcmp(td, "0") != 0)) {
+    if (fflush(stdout) != 0) {
+      perror("stdout");
+      return 1;
+    }
+    if (trace) fprintf(stderr, "ciruela-index: exit without cir_destroy\n");
+    fflush(stderr);
+    _exit(0);
+  }
   const auto t_destroy = std::chrono::steady_clock::now();
   cir_destroy(ctx);
   if (trace) fprintf(stderr, "ciruela-index: cir_destroy %.1f ms\n", ms_since(t_destroy));

@@ -4,7 +4,10 @@ only), of a bare HIP start-up (build/hip_start_probe), and of the sync of a
 100-file / 10 MiB tree with CIR_TRACE=1 (HIP runtime start, cir_init, the
 scan, cir_destroy as the CLI reports them).
 
-    python tools/cli_startup.py [--runs 5]
+    python tools/cli_startup.py [--runs 5] [--ab-teardown]
+
+--ab-teardown: only the sync, alternating the default exit (no cir_destroy)
+with CIR_CLI_TEARDOWN=1, without CIR_TRACE; prints each run and the medians.
 """
 import argparse
 import os
@@ -25,6 +28,7 @@ def timed(cmd, env=None):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--runs", type=int, default=5)
+    ap.add_argument("--ab-teardown", action="store_true")
     args = ap.parse_args()
     cli = os.path.join(ROOT, "bin", "ciruela-index")
     probe = os.path.join(ROOT, "build", "hip_start_probe")
@@ -35,6 +39,20 @@ def main():
             os.makedirs(d, exist_ok=True)
             with open(os.path.join(d, "f%03d" % i), "wb") as f:
                 f.write(os.urandom(100 << 10) if i < 99 else os.urandom((10 << 20) - 99 * (100 << 10)))
+        if args.ab_teardown:
+            runs = {"exit": [], "teardown": []}
+            for r in range(args.runs):
+                for mode in ("exit", "teardown"):
+                    env = dict(os.environ, CIR_CLI_TEARDOWN="1" if mode == "teardown" else "0")
+                    s, p = timed([cli, "sync", "--append", tree + ":/x"], env)
+                    if p.returncode:
+                        print(p.stderr)
+                        sys.exit(p.returncode)
+                    runs[mode].append(s * 1e3)
+                    print("%s %.1f ms | %s" % (mode, s * 1e3, p.stdout.split()[0]), flush=True)
+            for mode, v in runs.items():
+                print("median %s %.1f ms over %d runs" % (mode, sorted(v)[len(v) // 2], len(v)))
+            return
         for r in range(args.runs):
             s, _ = timed([cli])
             print("no-args (load only) %.1f ms" % (s * 1e3), flush=True)
