@@ -526,18 +526,49 @@ def test_memory_blocks(gpu, oracle):
         assert r.read_block(oracle_digest(oracle, blk)) == blk
 
 
-def test_cli_sync(gpu, tmp_path):
+@pytest.mark.parametrize("teardown", ["0", "1"])
+def test_cli_sync(gpu, tmp_path, teardown):
+    """One `ciruela-index sync` process; by default it leaves its context to
+    process exit (`_exit` after flushing), CIR_CLI_TEARDOWN=1 destroys it
+    first: both print the same line and write the same index."""
     import subprocess
     from conftest import ROOT
     make_tree(tmp_path / "src")
-    out = subprocess.check_output([os.path.join(ROOT, "bin", "ciruela-index"), "sync",
-                                   "--append", str(tmp_path / "src") + ":/dest",
-                                   "--index-dir", str(tmp_path)])
-    image_id, kind, dest, src = out.decode().split()
+    env = dict(os.environ, CIR_CLI_TEARDOWN=teardown)
+    p = subprocess.run([os.path.join(ROOT, "bin", "ciruela-index"), "sync",
+                        "--append", str(tmp_path / "src") + ":/dest",
+                        "--index-dir", str(tmp_path)], env=env, capture_output=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    image_id, kind, dest, src = p.stdout.decode().split()
     want = dirsig_oracle.scan(str(tmp_path / "src"), 32768)
     assert (tmp_path / (image_id + ".ds1")).read_bytes() == want
     assert kind == "append" and dest == "/dest"
     assert want.endswith(image_id.encode() + b"\n")
+    assert b"Indexed" in p.stderr
+
+
+def test_cli_hash(gpu, oracle, tmp_path):
+    """`ciruela-index hash FILE...` (the per-file Hashes::hash_file list):
+    every line -- path, size, one digest per block -- equal to the oracle,
+    through a pipe (stdout fully buffered, flushed before the process exits
+    without tearing its context down)."""
+    import subprocess
+    from conftest import ROOT
+    sizes = [0, 1, 4096, 4097, 3 * 4096 + 100]
+    paths = []
+    for i, n in enumerate(sizes):
+        f = tmp_path / ("f%d" % i)
+        f.write_bytes(os.urandom(n))
+        paths.append(str(f))
+    p = subprocess.run([os.path.join(ROOT, "bin", "ciruela-index"), "hash", "--block-size", "4096"]
+                       + paths, capture_output=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    lines = p.stdout.decode().splitlines()
+    assert len(lines) == len(paths)
+    for path, n, line in zip(paths, sizes, lines):
+        data = open(path, "rb").read()
+        want = [oracle_digest(oracle, data[k:k + 4096]).hex() for k in range(0, n, 4096)]
+        assert line.split() == [path, str(n)] + want, path
 
 
 def test_sha512_256_single_and_batches(gpu, ctx, oracle):
