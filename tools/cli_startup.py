@@ -29,6 +29,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--runs", type=int, default=5)
     ap.add_argument("--ab-teardown", action="store_true")
+    ap.add_argument("--ab-env", default="CIR_CLI_TEARDOWN",
+                    help="the variable --ab-teardown alternates between 0 and 1")
     args = ap.parse_args()
     cli = os.path.join(ROOT, "bin", "ciruela-index")
     probe = os.path.join(ROOT, "build", "hip_start_probe")
@@ -43,7 +45,7 @@ def main():
             runs = {"exit": [], "teardown": []}
             for r in range(args.runs):
                 for mode in ("exit", "teardown"):
-                    env = dict(os.environ, CIR_CLI_TEARDOWN="1" if mode == "teardown" else "0")
+                    env = dict(os.environ, **{args.ab_env: "1" if mode == "teardown" else "0"})
                     s, p = timed([cli, "sync", "--append", tree + ":/x"], env)
                     if p.returncode:
                         print(p.stderr)
@@ -51,7 +53,8 @@ def main():
                     runs[mode].append(s * 1e3)
                     print("%s %.1f ms | %s" % (mode, s * 1e3, p.stdout.split()[0]), flush=True)
             for mode, v in runs.items():
-                print("median %s %.1f ms over %d runs" % (mode, sorted(v)[len(v) // 2], len(v)))
+                print("median %s=%s %.1f ms over %d runs" % (args.ab_env, "1" if mode == "teardown" else "0",
+                                                         sorted(v)[len(v) // 2], len(v)))
             return
         for r in range(args.runs):
             s, _ = timed([cli])
