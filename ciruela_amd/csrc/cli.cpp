@@ -218,11 +218,13 @@ int main(int argc, char** argv) {
       if (!index_dir.empty()) {
         const std::string p = index_dir + "/" + hex(id, idl) + ".ds1";
         FILE* f = fopen(p.c_str(), "wb");
-        if (!f || fwrite(index, 1, len, f) != len) {
+        // (a full disk can surface only at fclose, when the buffer is written)
+        const bool ok = f && fwrite(index, 1, len, f) == len;
+        if (!ok || (f && fclose(f) != 0)) {
           perror(p.c_str());
+          if (!ok && f) fclose(f);
           return 1;
         }
-        fclose(f);
       }
       cir_free(index);
     }
