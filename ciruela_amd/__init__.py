@@ -58,10 +58,20 @@ def _buf(data):
 class Context:
     """A cir_ctx: the devices the host-memory entry points run on."""
 
-    def __init__(self, device_mask=0, staging_bytes=0):
+    def __init__(self, device_mask=0, staging_bytes=0, max_devices=0):
+        """max_devices: open at most that many of the masked devices (0 = all;
+        cir_init_n).  devices_for_bytes() gives the count an input can use."""
         h = ctypes.c_void_p()
-        _n.check(_n.lib.cir_init(ctypes.byref(h), device_mask, staging_bytes))
+        _n.check(_n.lib.cir_init_n(ctypes.byref(h), device_mask, staging_bytes, max_devices))
         self._h = h
+
+    @staticmethod
+    def devices_for_bytes(work_bytes, staging_bytes=0, visible=None):
+        """cir_devices_for_bytes: ceil(work / (2 x staging)) capped at the
+        visible count (no HIP call when `visible` is given)."""
+        if visible is None:
+            visible = _n.lib.cir_device_count()
+        return _n.lib.cir_devices_for_bytes(work_bytes, staging_bytes, visible)
 
     @property
     def handle(self):
@@ -196,6 +206,26 @@ class Context:
 
     def verify_window(self, window_us, max_batch=4096):
         _n.check(_n.lib.cir_verify_window(self._h, window_us, max_batch))
+
+    def verify_forget(self, ticket):
+        """Drop a ticket (pending or finished) whose outcome is not wanted."""
+        _n.check(_n.lib.cir_verify_forget(self._h, ticket))
+
+    def verify_limits(self, max_bytes=0, max_results=0, nonblocking=False):
+        """Bound the queue (block bytes accepted, not yet verified) and the
+        outcomes held; 0 = the library default.  nonblocking: a submit that
+        would pass max_bytes raises CiruelaError(CIR_EAGAIN) instead of
+        waiting."""
+        _n.check(_n.lib.cir_verify_limits(self._h, max_bytes, max_results,
+                                          _n.CIR_VERIFY_NONBLOCK if nonblocking else 0))
+
+    VERIFY_STATS_FIELDS = ("bytes_held", "peak_bytes_held", "pending", "outcomes_held",
+                           "expired", "forgotten", "refused", "batches")
+
+    def verify_stats(self):
+        out = (ctypes.c_uint64 * _n.CIR_VERIFY_STATS_FIELDS)()
+        _n.check(_n.lib.cir_verify_stats(self._h, out))
+        return dict(zip(self.VERIFY_STATS_FIELDS, list(out)))
 
     def check_file(self, fd, block_size, expected, hash_type=None):
         ht = (hash_type or HashType.blake2b_256()).code

@@ -43,6 +43,9 @@ CIR_ENOTFOUND = -6
 CIR_EHASHSIZE = -7
 CIR_ENODEV = -8
 CIR_EUNSUPPORTED = -9
+CIR_EAGAIN = -10
+CIR_VERIFY_NONBLOCK = 1
+CIR_VERIFY_STATS_FIELDS = 8
 CIR_STAGING_LAZY = (1 << 64) - 1  # cir_init: no staging slots until a host path needs them
 
 CIR_HASH_BLAKE2B_256 = 1
@@ -54,6 +57,9 @@ WRITE_FN = ctypes.CFUNCTYPE(ctypes.c_int, c_vp, c_vp, ctypes.c_size_t)
 # name -> (restype, argtypes)
 _SIGS = {
     "cir_init": (ctypes.c_int, [ctypes.POINTER(c_vp), ctypes.c_uint32, ctypes.c_uint64]),
+    "cir_init_n": (ctypes.c_int, [ctypes.POINTER(c_vp), ctypes.c_uint32, ctypes.c_uint64,
+                                  ctypes.c_uint32]),
+    "cir_devices_for_bytes": (ctypes.c_uint32, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]),
     "cir_destroy": (None, [c_vp]),
     "cir_device_count": (ctypes.c_int, []),
     "cir_ctx_devices": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
@@ -118,6 +124,9 @@ _SIGS = {
     "cir_verify_poll": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_int)]),
     "cir_verify_wait": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_int)]),
     "cir_verify_window": (ctypes.c_int, [c_vp, ctypes.c_uint32, ctypes.c_uint32]),
+    "cir_verify_forget": (ctypes.c_int, [c_vp, ctypes.c_uint64]),
+    "cir_verify_limits": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int]),
+    "cir_verify_stats": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_uint64)]),
     "cir_set_footer_mode": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "cir_debug_scan_timing": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "cir_debug_scan_batches": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double),

@@ -75,14 +75,21 @@ static uint64_t tree_bytes(const std::string& path, uint64_t cap, uint64_t acc =
   return acc;
 }
 
+// Bytes of every input, counted up to what decides the device count: two
+// default staging slots per device for 32 devices (cir_devices_for_bytes).
+static uint64_t input_bytes(const std::vector<std::string>& paths) {
+  constexpr uint64_t kCap = 32 * 2 * (256ull << 20);
+  uint64_t total = 0;
+  for (const std::string& p : paths) total = tree_bytes(p, kCap, total);
+  return total;
+}
+
 // Staging per slot: the library default (256 MiB) for large inputs; a small
 // input gets slots just big enough to hold it, so a one-shot `sync` of a few
 // MiB does not pin 3 x 256 MiB of host memory it never fills (cir_init
 // allocates the slots up front).
-static uint64_t staging_for(const std::vector<std::string>& paths) {
+static uint64_t staging_for(uint64_t total) {
   constexpr uint64_t kMax = 256ull << 20, kMin = 1ull << 20;
-  uint64_t total = 0;
-  for (const std::string& p : paths) total = tree_bytes(p, kMax, total);
   if (total >= kMax) return 0;
   return std::max<uint64_t>(kMin, (total + kMin - 1) / kMin * kMin);
 }
@@ -148,7 +155,8 @@ int main(int argc, char** argv) {
   std::vector<std::string> inputs = files;
   for (const Job& j : jobs) inputs.push_back(j.src);
   cir_ctx* ctx = nullptr;
-  const uint64_t staging = staging_for(inputs);
+  const uint64_t total = input_bytes(inputs);
+  const uint64_t staging = staging_for(total);
   const char* tv = getenv("CIR_TRACE");
   const bool trace = tv && *tv && strcmp(tv, "0") != 0;
   auto ms_since = [](std::chrono::steady_clock::time_point t) {
@@ -162,14 +170,21 @@ int main(int argc, char** argv) {
     const int n = cir_device_count();
     fprintf(stderr, "ciruela-index: HIP runtime start %.1f ms (%d devices)\n", ms_since(t0), n);
   }
-  // an input below one staging slot (256 MiB) is one batch on one GPU: open
-  // only the first visible device instead of every GPU of the node (each
-  // costs its device context, streams and pinned staging at start-up)
-  const uint32_t mask = staging ? 1u : 0u;
+  // open only the GPUs the input can use: one per two staging batches of it
+  // (cir_devices_for_bytes), the lowest-numbered first -- a tree below one
+  // slot (256 MiB) is one batch on one GPU -- instead of every GPU of the
+  // node (each costs its device context, streams and 834 MiB of pinned
+  // staging at start-up, include/ciruela_blockhash.h)
+  const uint32_t ndev = cir_devices_for_bytes(total, staging, 32);
   const auto t_init = std::chrono::steady_clock::now();
-  int rc = cir_init(&ctx, mask, staging);
+  int rc = cir_init_n(&ctx, 0, staging, ndev);
   if (rc) return die(rc, "cir_init");
-  if (trace) fprintf(stderr, "ciruela-index: cir_init %.1f ms\n", ms_since(t_init));
+  if (trace) {
+    int ids[64];
+    const int opened = cir_ctx_devices(ctx, ids, 64);
+    fprintf(stderr, "ciruela-index: cir_init %.1f ms, %d device(s) for %llu input bytes\n",
+            ms_since(t_init), opened, (unsigned long long)total);
+  }
   if (cmd == "hash") {
     for (const std::string& f : files) {
       const int fd = open(f.c_str(), O_RDONLY);

@@ -33,6 +33,7 @@
 #include "blake2b_host.hpp"
 #include "dirsig.hpp"
 #include "sha512_host.hpp"
+#include "stripes.hpp"
 #include "runtime.hpp"
 
 namespace cir {
@@ -385,7 +386,8 @@ static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, u
   uint64_t stripe = std::max<uint64_t>(1, ctx->staging / bs);
   if (const char* e = getenv("CIR_DEBUG_STRIPE_BLOCKS"))  // tests: stripes of a few blocks
     if (atoll(e) > 0) stripe = (uint64_t)atoll(e);
-  const size_t nstripes = (size_t)((nblk_total + stripe - 1) / stripe);
+  StripePrefix order(nblk_total, stripe);
+  const size_t nstripes = order.stripes();
   std::vector<BlockRanges> dev_ranges(nd);
   std::vector<std::vector<size_t>> global_index(nd);  // (device, range) -> stripe
   for (size_t st = 0; st < nstripes; ++st) {
@@ -393,22 +395,14 @@ static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, u
     dev_ranges[i].push_back({st * stripe, std::min<uint64_t>((st + 1) * stripe, nblk_total)});
     global_index[i].push_back(st);
   }
-  std::vector<uint64_t> got(nstripes, 0);
-  size_t first_open = 0;  // first stripe not yet complete
   std::mutex mu;
   const int dev0 = ctx->devs[0]->id;
   auto done = [&](size_t i, size_t r, uint64_t n) -> int {
     std::lock_guard<std::mutex> lk(mu);
-    const size_t st = global_index[i][r];
-    got[st] = n;
-    const uint64_t before = first_open < nstripes ? first_open * stripe + got[first_open]
-                                                  : nblk_total;
-    while (first_open < nstripes &&
-           got[first_open] == std::min<uint64_t>(stripe, nblk_total - first_open * stripe))
-      ++first_open;
-    const uint64_t prefix = first_open < nstripes ? first_open * stripe + got[first_open]
-                                                  : nblk_total;
-    if (prefix == before) return CIR_OK;  // this batch did not extend the prefix
+    uint64_t prefix = 0;
+    // (a batch inside the first open stripe extends the prefix too, and so
+    // does the last stripe's completion)
+    if (!order.update(global_index[i][r], n, &prefix)) return CIR_OK;
     int cur = 0;
     CIR_HIP(hipGetDevice(&cur));
     CIR_HIP(hipSetDevice(dev0));

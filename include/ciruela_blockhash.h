@@ -60,7 +60,8 @@ enum cir_status {
   CIR_ENOTFOUND = -6,  /* ReadError::NotFound (src/index.rs:78, src/blocks.rs:101) */
   CIR_EHASHSIZE = -7,  /* DirError::HashSize (src/blocks.rs:123) */
   CIR_ENODEV = -8,     /* no usable gfx950 device */
-  CIR_EUNSUPPORTED = -9 /* reserved (every dir-signature hash type is implemented) */
+  CIR_EUNSUPPORTED = -9, /* reserved (every dir-signature hash type is implemented) */
+  CIR_EAGAIN = -10       /* cir_verify_submit, non-blocking: the verify queue is full */
 };
 
 /* dir-signature HashType (external crate 0.2.9; header tokens in the index) */
@@ -80,16 +81,35 @@ typedef struct cir_ctx cir_ctx;
  * its streams (compute, copy, quad part, footer chain), the relay scratch,
  * the ordering scratch for one full staging batch and -- unless staging_bytes
  * is CIR_STAGING_LAZY -- three staging slots (pinned host + device memory of
- * staging_bytes each, plus descriptor and digest buffers: about 3 x
- * staging_bytes of pinned host memory and as much VRAM, 768 MiB each at the
- * default).  A tiny warm-up hash loads the kernels and the first copies on the
- * staging and chain streams are paid here.  Allocated later, on first use:
- * the footer-chain text buffers (cir_scan_v1 with CIR_FOOTER_GPU), the
- * single-launch buffers of cir_blake2b256, timing events, and -- with
- * CIR_STAGING_LAZY -- the staging slots (256 MiB each), so a context used only
- * through the *_dev entry points pins no staging memory. */
+ * staging_bytes each, plus descriptor and digest buffers).  A tiny warm-up
+ * hash loads the kernels and the first copies on the staging and chain
+ * streams are paid here.  Allocated later, on first use: the footer-chain
+ * text buffers (cir_scan_v1 with CIR_FOOTER_GPU), the single-launch buffers
+ * of cir_blake2b256, timing events, and -- with CIR_STAGING_LAZY -- the
+ * staging slots (256 MiB each), so a context used only through the *_dev
+ * entry points pins no staging memory.
+ *
+ * Cost per opened device, staging S (blocks per slot B = max(S / 512, 4096)):
+ *   pinned host memory  3 x (S + 44 B)            = 834 MiB at the default
+ *   device memory       3 x (S + 44 B) + 8 B + 4 MiB (ordering, relay)
+ *                                                 = 842 MiB at the default
+ *   with CIR_STAGING_LAZY: ~4.2 MiB of device memory and no pinned memory
+ *   until a host path runs; plus, either way, the HIP runtime's own context
+ *   on that device and cir_init's 0.1-0.3 s of start-up. */
 #define CIR_STAGING_LAZY ((uint64_t)-1)
 int cir_init(cir_ctx** ctx, uint32_t device_mask, uint64_t staging_bytes);
+/* cir_init with a device-count hint: opens at most max_devices of the
+ * devices device_mask selects, the lowest-numbered first (0 = no cap, as
+ * cir_init).  With cir_devices_for_bytes a caller that knows how much input
+ * it will stage opens only the devices that input can use. */
+int cir_init_n(cir_ctx** ctx, uint32_t device_mask, uint64_t staging_bytes, uint32_t max_devices);
+/* The devices worth opening for work_bytes of host-path input (a scan's
+ * tree, a hash_file / hash_memory input): ceil(work_bytes / (2 x staging))
+ * -- each device gets at least two staging batches, so its start-up and
+ * pinned slots are not spent on a fraction of one -- capped at `visible`,
+ * at least 1; work_bytes == 0 (unknown) gives `visible`.  staging_bytes as
+ * cir_init's (0 / CIR_STAGING_LAZY = 256 MiB).  Pure: no HIP call. */
+uint32_t cir_devices_for_bytes(uint64_t work_bytes, uint64_t staging_bytes, uint32_t visible);
 void cir_destroy(cir_ctx* ctx);
 int cir_device_count(void);
 /* devices opened by ctx; ids[i] receives the HIP ordinal of the i-th. */
@@ -176,20 +196,46 @@ int cir_verify_blocks(cir_ctx* ctx, int hash_type, const uint8_t* h_arena, const
 
 /* The same check one block at a time, asynchronously, for a caller that
  * receives blocks one by one (FetchBlock::poll, fetch_blocks.rs:77):
- * cir_verify_submit copies the block and its expected digest and returns a
- * ticket at once; a worker thread of the context verifies what was
- * submitted within a short window (default 200 us after the first waiting
- * block, at most 4096 blocks, one hash type per batch) as one host batch.
- * cir_verify_poll: *state = 0 pending, 1 match, 2 mismatch (the outcome is
- * consumed when reported).  cir_verify_wait blocks: *ok = 1 match, 0
- * mismatch.  A failed batch returns its error for each of its tickets; an
- * unknown or consumed ticket is CIR_ENOTFOUND.  cir_verify_window sets the
- * window (microseconds) and the batch cap. */
+ * cir_verify_submit copies the block (once, into the arena of the batch
+ * being formed) with its expected digest and returns a ticket; a worker
+ * thread of the context verifies each batch as one host batch once it is full
+ * or a short window after its first block (default 200 us, at most 4096
+ * blocks, one hash type per batch).  cir_verify_poll: *state = 0 pending,
+ * 1 match, 2 mismatch (the outcome is consumed when reported).
+ * cir_verify_wait blocks: *ok = 1 match, 0 mismatch.  A failed batch returns
+ * its error for each of its tickets.  An unknown, consumed, forgotten or
+ * expired ticket is CIR_ENOTFOUND.  cir_verify_window sets the window
+ * (microseconds) and the batch cap.
+ *
+ * Bounds (cir_verify_limits; 0 = the default):
+ *   max_bytes    block bytes accepted and not yet verified (default 256 MiB;
+ *                a batch's arena holds at most half of it).  A submit that
+ *                would pass it waits until the worker has verified enough,
+ *                or with flags = CIR_VERIFY_NONBLOCK returns CIR_EAGAIN (the
+ *                block is not taken: retry later or elsewhere).  A block
+ *                larger than max_bytes is taken once nothing else is held.
+ *   max_results  finished outcomes held for tickets not yet polled, waited
+ *                or forgotten (default 2^20); beyond it the oldest tickets'
+ *                outcomes are dropped (they become CIR_ENOTFOUND, counted as
+ *                expired).
+ * cir_verify_forget drops a ticket the caller no longer wants (a block the
+ * reference would re-fetch elsewhere, :91-103): a pending one is still
+ * hashed with its batch but its outcome is never held; a finished one's
+ * outcome is released.
+ * cir_verify_stats: out[0] bytes held (accepted, not yet verified), [1] the
+ * peak of [0], [2] pending tickets, [3] outcomes held, [4] outcomes
+ * expired, [5] tickets forgotten, [6] submits refused with CIR_EAGAIN,
+ * [7] batches verified. */
+#define CIR_VERIFY_NONBLOCK 1
+#define CIR_VERIFY_STATS_FIELDS 8
 int cir_verify_submit(cir_ctx* ctx, int hash_type, const uint8_t* data, size_t n,
                       const uint8_t expected[CIR_DIGEST_BYTES], uint64_t* ticket);
 int cir_verify_poll(cir_ctx* ctx, uint64_t ticket, int* state);
 int cir_verify_wait(cir_ctx* ctx, uint64_t ticket, int* ok);
+int cir_verify_forget(cir_ctx* ctx, uint64_t ticket);
 int cir_verify_window(cir_ctx* ctx, uint32_t window_us, uint32_t max_batch);
+int cir_verify_limits(cir_ctx* ctx, uint64_t max_bytes, uint64_t max_results, int flags);
+int cir_verify_stats(cir_ctx* ctx, uint64_t out[CIR_VERIFY_STATS_FIELDS]);
 
 /* Hashes::check_file(&mut file) at image commit (src/daemon/disk/commit.rs:
  * 104; false -> Error::Checksum, :110): re-hash fd from its current offset to

@@ -60,9 +60,32 @@ def test_library_is_gfx950_code():
 
 
 def test_strerror_codes():
-    for code in range(-9, 1):
+    for code in range(-10, 1):
         assert _native.lib.cir_strerror(code)
     assert _native.lib.cir_strerror(_native.CIR_ENOTFOUND) == b"not found"
+    assert _native.lib.cir_strerror(_native.CIR_EAGAIN) == b"try again"
+
+
+def test_device_count_policy():
+    """cir_devices_for_bytes (the CLI's and cir_init_n's device-count hint,
+    no HIP call): ceil(bytes / (2 x staging)) devices, capped at the visible
+    count, at least one; unknown work (0) opens every visible device."""
+    f = _native.lib.cir_devices_for_bytes
+    MiB, GiB = 1 << 20, 1 << 30
+    assert f(10 * MiB, 10 * MiB, 8) == 1          # the config-1 CLI: one slot, one GPU
+    assert f(300 * MiB, 0, 8) == 1                # default staging 256 MiB: 2 x 256 per GPU
+    assert f(512 * MiB, 0, 8) == 1
+    assert f(512 * MiB + 1, 0, 8) == 2
+    assert f(520 * MiB, _native.CIR_STAGING_LAZY, 8) == 2
+    assert f(3 * GiB, 0, 8) == 6
+    assert f(50 * GiB, 0, 8) == 8                 # config 5 on a node: every GPU
+    assert f(50 * GiB, 0, 1) == 1
+    assert f(1, 0, 8) == 1
+    assert f(0, 0, 8) == 8 and f(0, 0, 3) == 3
+    assert f(5 * GiB, 0, 0) == 0
+    assert f(100 * MiB, 16 * MiB, 32) == 4        # small slots: more devices per byte
+    assert f((1 << 64) - 1, (1 << 63), 4) == 1    # no overflow in 2 x staging
+    assert ca.Context.devices_for_bytes(3 * GiB, visible=4) == 4
 
 
 def test_no_device_is_loud():

@@ -571,6 +571,47 @@ def test_cli_hash(gpu, oracle, tmp_path):
         assert line.split() == [path, str(n)] + want, path
 
 
+@pytest.mark.parametrize("mib,states", [(300, 1), (520, 2)])
+def test_cli_opens_devices_for_its_input(gpu, tmp_path, mib, states):
+    """`ciruela-index sync` opens ceil(input / (2 x 256 MiB)) devices
+    (cir_devices_for_bytes + cir_init_n), not every GPU of the node: on the
+    one-GPU box CIR_DEBUG_SPLIT=4 offers four device states, and a 300 MiB
+    tree takes one, a 520 MiB tree two.  The index is the scan oracle's
+    either way (sparse files: the bytes are zeros, the sizes are real)."""
+    import subprocess
+    from conftest import ROOT
+    src = tmp_path / "src"
+    (src / "d").mkdir(parents=True)
+    per = (mib << 20) // 4
+    for k in range(4):
+        with open(src / "d" / ("f%d" % k), "wb") as f:
+            f.truncate(per + 1000 * k)
+    env = dict(os.environ, CIR_DEBUG_SPLIT="4", CIR_TRACE="1")
+    p = subprocess.run([os.path.join(ROOT, "bin", "ciruela-index"), "sync",
+                        "--append", str(src) + ":/dest", "--index-dir", str(tmp_path)],
+                       env=env, capture_output=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [ln for ln in p.stderr.decode().splitlines() if "device(s) for" in ln]
+    assert line and (" %d device(s) for %d input bytes" % (states, 4 * per + 6000)) in line[0], \
+        line
+    image_id = p.stdout.decode().split()[0]
+    want = dirsig_oracle.scan(str(src), 32768)
+    assert (tmp_path / (image_id + ".ds1")).read_bytes() == want
+
+
+def test_context_device_hint(gpu, monkeypatch):
+    """cir_init_n: at most max_devices of the masked device states."""
+    monkeypatch.setenv("CIR_DEBUG_SPLIT", "3")
+    c = gpu.Context(device_mask=1, staging_bytes=1 << 20, max_devices=2)
+    c0 = gpu.Context(device_mask=1, staging_bytes=1 << 20)
+    monkeypatch.delenv("CIR_DEBUG_SPLIT")
+    assert len(c.devices()) == 2 and len(c0.devices()) == 3
+    data = os.urandom(3 << 20)
+    assert c.hash_memory(data, 32768) == c0.hash_memory(data, 32768)
+    c.close()
+    c0.close()
+
+
 def test_sha512_256_single_and_batches(gpu, ctx, oracle):
     """dir-signature's second hash type on the GPU vs the oracle."""
     import torch
@@ -1063,6 +1104,47 @@ def test_multi_device_split_paths(gpu, oracle, tmp_path):
                 assert gpu.v1.scan(cfg, context=ctx) == want, (block_size, mode, 3)
             finally:
                 del os.environ["CIR_DEBUG_STRIPE_BLOCKS"]
+
+
+class _CountingSink(bytearray):
+    """A bytearray that counts the writer calls cir_scan_v1_write made."""
+    writes = 0
+
+    def extend(self, b):
+        self.writes += 1
+        super().extend(b)
+
+
+def test_split_scan_streams_within_stripes(gpu, monkeypatch, tmp_path):
+    """A scan over two device states whose stripes take several batches
+    each: every batch that extends the complete prefix reaches the emitter
+    (stripes.hpp), so the index is written in many pieces while stripe 0 is
+    still open -- before, a batch inside the first open stripe was never
+    reported and the sink saw only the header, stripe completions and the
+    tail.  128 one-block files in one directory, stripes of 64 blocks, 64 KiB
+    staging slots (16 blocks; ramped 2, 4, 8, 16): stripe 0 alone takes >= 5
+    batches on device state 0.  Index = the scan oracle's."""
+    monkeypatch.setenv("CIR_DEBUG_SPLIT", "2")
+    c = gpu.Context(device_mask=1, staging_bytes=64 << 10)
+    monkeypatch.delenv("CIR_DEBUG_SPLIT")
+    assert len(c.devices()) == 2
+    rng = random.Random(64)
+    tree = tmp_path / "tree" / "d"
+    tree.mkdir(parents=True)
+    for k in range(128):
+        (tree / ("f%03d" % k)).write_bytes(rng.randbytes(4096))
+    root = str(tmp_path / "tree")
+    want = dirsig_oracle.scan(root, 4096)
+    monkeypatch.setenv("CIR_DEBUG_STRIPE_BLOCKS", "64")
+    cfg = gpu.ScannerConfig.new().block_size(4096).threads(2).add_dir(root, "/")
+    for mode in (c.FOOTER_HOST, c.FOOTER_GPU):
+        c.set_footer_mode(mode)
+        sink = _CountingSink()
+        n = c.scan_into(cfg, sink)
+        assert bytes(sink) == want and n == len(want), mode
+        # >= 5 batches of stripe 0 + the last emit / footer line
+        assert sink.writes >= 6, (mode, sink.writes)
+    c.close()
 
 
 def test_error_paths_are_codes_not_aborts(gpu, small_ctx, tmp_path):
@@ -1799,6 +1881,139 @@ def test_verify_async_blocks_share_batches(gpu, oracle):
     print("async verify: 256 x 32 KiB in %.2f ms (%.1f us/block); one drop-in call %.0f us"
           % (both * 1e3, both * 1e6 / 256, one * 1e6))
     assert both < 0.25 * 256 * one, (both, one)
+    c.close()
+
+
+def _blocks_with_bad(oracle, rng, n, size=32768, every=5):
+    """n random blocks, their oracle digests, one in `every` expected digest
+    corrupted: [(data, expected, good)]."""
+    out = []
+    for i in range(n):
+        data = rng.randbytes(size)
+        want = oracle_digest(oracle, data)
+        good = i % every != 2
+        out.append((data, want if good else bytes([want[0] ^ 0x40]) + want[1:], good))
+    return out
+
+
+def test_verify_async_queue_is_bounded(gpu, oracle):
+    """cir_verify_limits: the block bytes accepted and not yet verified never
+    pass max_bytes.  Non-blocking, a submit that would pass it is CIR_EAGAIN
+    and the block is not taken (deterministic here: the first block's batch
+    waits out a 100 ms window); blocking, submitters from three threads wait
+    for room.  Every accepted ticket resolves to the oracle's outcome, wrong
+    digests included, and nothing stays held."""
+    import threading
+    n = gpu._n
+    c = gpu.Context(device_mask=1, staging_bytes=16 << 20)
+    rng = random.Random(77)
+    # non-blocking: 64 KiB bound, 40 KiB blocks, a 100 ms window
+    c.verify_limits(max_bytes=64 << 10, nonblocking=True)
+    c.verify_window(100000)
+    a, b = _blocks_with_bad(oracle, rng, 2, size=40 << 10, every=2)  # b's digest is wrong
+    ta = c.verify_submit(a[0], a[1])
+    with pytest.raises(n.CiruelaError) as e:
+        c.verify_submit(b[0], b[1])
+    assert e.value.status == n.CIR_EAGAIN
+    t_empty = c.verify_submit(b"", oracle_digest(oracle, b""))  # 0 bytes always fit
+    st = c.verify_stats()
+    assert st["refused"] == 1 and st["bytes_held"] == 40 << 10 and st["pending"] == 2
+    assert c.verify_wait(ta) is True and c.verify_wait(t_empty) is True
+    tb = c.verify_submit(b[0], b[1])  # room again
+    assert c.verify_wait(tb) is False
+    # a burst through a 1 MiB bound, non-blocking with retries, then blocking
+    c.verify_window(200)
+    c.verify_limits(max_bytes=1 << 20, nonblocking=True)
+    items = _blocks_with_bad(oracle, rng, 600)
+    tickets = []
+    for data, exp, _ in items:
+        while True:
+            try:
+                tickets.append(c.verify_submit(data, exp))
+                break
+            except n.CiruelaError as ex:
+                assert ex.status == n.CIR_EAGAIN
+    assert [c.verify_wait(t) for t in tickets] == [g for _, _, g in items]
+    st = c.verify_stats()
+    print("non-blocking burst: %d refusals, peak %d bytes" % (st["refused"], st["peak_bytes_held"]))
+    assert st["peak_bytes_held"] <= 1 << 20
+    c.verify_limits(max_bytes=1 << 20)  # blocking
+    items = _blocks_with_bad(oracle, rng, 900)
+    tickets = [None] * len(items)
+
+    def submit(part):
+        for i in range(part, len(items), 3):
+            tickets[i] = c.verify_submit(items[i][0], items[i][1])
+    th = [threading.Thread(target=submit, args=(p,)) for p in range(3)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert [c.verify_wait(t) for t in tickets] == [g for _, _, g in items]
+    st = c.verify_stats()
+    assert st["peak_bytes_held"] <= 1 << 20, st
+    assert st["bytes_held"] == 0 and st["pending"] == 0 and st["outcomes_held"] == 0, st
+    c.close()
+
+
+def test_verify_async_forget_and_expiry(gpu, oracle):
+    """cir_verify_forget drops a pending ticket (its outcome is never held; a
+    thread waiting on it is released with NotFound) and a finished one;
+    cir_verify_limits(max_results) keeps only the newest outcomes, the oldest
+    expire (NotFound) -- and the outcomes kept still match the oracle."""
+    import threading
+    n = gpu._n
+    c = gpu.Context(device_mask=1, staging_bytes=16 << 20)
+    rng = random.Random(78)
+    items = _blocks_with_bad(oracle, rng, 8, size=4096, every=3)
+    # a pending ticket (100 ms window), forgotten
+    c.verify_window(100000)
+    t1 = c.verify_submit(items[0][0], items[0][1])
+    c.verify_forget(t1)
+    with pytest.raises(n.CiruelaError) as e:
+        c.verify_poll(t1)
+    assert e.value.status == n.CIR_ENOTFOUND
+    # forgotten while another thread waits on it
+    t2 = c.verify_submit(items[1][0], items[1][1])
+    got = []
+
+    def waiter():
+        try:
+            got.append(c.verify_wait(t2))
+        except n.CiruelaError as ex:
+            got.append(ex.status)
+    w = threading.Thread(target=waiter)
+    w.start()
+    import time
+    time.sleep(0.02)
+    c.verify_forget(t2)
+    w.join(10)
+    assert got == [n.CIR_ENOTFOUND]
+    # finished tickets: forget one, the other keeps its outcome
+    c.verify_window(0)
+    t3 = c.verify_submit(items[2][0], items[2][1])  # wrong digest
+    t4 = c.verify_submit(items[3][0], items[3][1])
+    assert c.verify_wait(t4) is True
+    c.verify_forget(t3)
+    for bad in (t3, t1, 987654321):
+        with pytest.raises(n.CiruelaError) as e:
+            c.verify_forget(bad)
+        assert e.value.status == n.CIR_ENOTFOUND
+    st = c.verify_stats()
+    assert st["forgotten"] == 3 and st["pending"] == 0 and st["outcomes_held"] == 0, st
+    # expiry: at most 16 outcomes held; the newest are kept and still right
+    c.verify_limits(max_results=16)
+    items = _blocks_with_bad(oracle, rng, 64, size=4096)
+    tickets = [c.verify_submit(d, x) for d, x, _ in items]
+    assert c.verify_wait(tickets[-1]) == items[-1][2]  # FIFO: every batch is done
+    st = c.verify_stats()
+    assert st["outcomes_held"] <= 16 and st["expired"] >= 64 - 1 - 16, st
+    with pytest.raises(n.CiruelaError) as e:
+        c.verify_poll(tickets[0])
+    assert e.value.status == n.CIR_ENOTFOUND
+    for i in range(64 - 16, 63):
+        assert c.verify_poll(tickets[i]) == items[i][2], i
+    assert c.verify_stats()["outcomes_held"] == 0
     c.close()
 
 
