@@ -94,6 +94,9 @@ def parse():
                    help="config 5: the index appended to a bytearray as the scan writes it "
                         "(cir_scan_v1_write, the reference's v1::scan into a Vec) or returned "
                         "whole (cir_scan_v1) and copied out")
+    p.add_argument("--dry-run-shared-device", action="store_true",
+                   help="--dry-run only: every rank reports the same device identity (the "
+                        "devices_seen check must fail the line under --dist-backend nccl)")
     p.add_argument("--dry-run-bad-rank", type=int, default=-1,
                    help="--dry-run only: this rank corrupts one digest of its shard (the "
                         "job-wide parity reduction must report FAIL)")
@@ -311,6 +314,55 @@ def job_parity(rows, reasons=None):
     if reasons:
         msg += " (%s)" % reasons
     return msg, checked
+
+
+def device_identity(ca, device_index):
+    """This rank's GPU as its driver and its own counters see it
+    (cir_debug_device_identity): PCI bus id, UUID, and one wave's reads of
+    the device's wall clock (s_memrealtime) and of its s_memtime counter
+    ~100 us apart -- the wall clock's value is the device's own (GPUs of one
+    node do not share it), and the counter rate is that GPU's clock."""
+    bus = ctypes.create_string_buffer(64)
+    uuid = ctypes.create_string_buffer(16)
+    clk = (ctypes.c_uint64 * 5)()
+    ca._n.check(ca._n.lib.cir_debug_device_identity(device_index, bus, 64, uuid, clk))
+    rt0, rt1, c0, c1, khz = list(clk)
+    wall_s = (rt1 - rt0) / (khz * 1e3) if khz and rt1 > rt0 else None
+    return {"hip_device": device_index, "pci_bus_id": bus.value.decode(),
+            "uuid": uuid.raw.hex(), "wall_clock_ticks": rt0, "wall_clock_khz": khz,
+            "memtime_mhz": round((c1 - c0) / wall_s / 1e6, 1) if wall_s else None}
+
+
+def gather_objects(obj):
+    """Every rank's `obj`, rank order, on every rank (all_gather_object over
+    the process group; [obj] without one)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        out = [None] * dist.get_world_size()
+        dist.all_gather_object(out, obj)
+        return out
+    return [obj]
+
+
+def devices_check(idents, one_device_per_rank):
+    """(distinct, problem) over every rank's device identity: two ranks on
+    one device (same PCI bus id or UUID) make the job's N GPUs fewer than N.
+    With RCCL (one_device_per_rank) that fails the line; gloo rehearsals with
+    shared GPUs only say so."""
+    seen, shared = {}, []
+    for r, d in enumerate(idents):
+        for key in ("pci_bus_id", "uuid"):
+            v = d.get(key)
+            if v:
+                if (key, v) in seen and seen[(key, v)] != r:
+                    shared.append((seen[(key, v)], r, v))
+                seen.setdefault((key, v), r)
+    if not shared:
+        return True, None
+    pairs = sorted({(a, b) for a, b, _ in shared})
+    msg = "ranks %s share a device (%s)" % (
+        ", ".join("%d/%d" % p for p in pairs), shared[0][2])
+    return False, ("FAIL: " + msg) if one_device_per_rank else msg
 
 
 def config4_check(oracle_lib, digests, nbytes, bs, first_block, sample=64):
@@ -682,20 +734,23 @@ def scan_batch_summary(batches, phases):
 
 
 def run_config5(args, ca, ctx, ctx_init_s=None):
-    """value = best of the scans; value_first = the first scan of this
-    process, which is what one `ciruela sync` sees (it scans once per run,
-    src/client/sync/mod.rs:192-201).  A tmpfs tree that was just written
-    reads ~6x slower the first time, for any reader (tools/first_read_probe.py:
-    a plain 16-thread CPU read pass 16 GiB/s first, 100-150 after); that
-    cost is paid here by one timed CPU read pass (tree_first_read) before the
-    scans, so seconds_first is the library's first scan, not the OS's first
-    touch of fresh pages."""
+    """value = best of the scans; value_first = the first timed scan of
+    this process, which is what one `ciruela sync` sees (it scans once per
+    run, src/client/sync/mod.rs:192-201) of a tree the page cache already
+    holds; value_cold = one scan of the tree right after this process wrote
+    it (when it did), before any other read.  A tmpfs tree that was just
+    written reads ~6x slower the first time, for any reader
+    (tools/first_read_probe.py: a plain 16-thread CPU read pass 16 GiB/s
+    first, 100-150 after), so the cold scan measures that first touch; two
+    timed CPU read passes (tree_first_read) follow it, before the timed
+    scans."""
+    fresh = getattr(args, "tree_fresh", None)
+    if fresh is None:
+        fresh = not tree_complete(args.tree_dir, args.tree_gib)
     t0 = time.perf_counter()
     nfiles = make_tree(args.tree_dir, args.tree_gib)
     gen_s = time.perf_counter() - t0
     nbytes = nfiles * 32 * (1 << 20)
-    rd_bytes, rd_s = tree_read_pass(args.tree_dir)
-    rd2_bytes, rd2_s = tree_read_pass(args.tree_dir)
     # reader threads: the library's own choice (auto_threads: min(12, 3/4 of
     # the process's CPU share), DESIGN.md 5) unless CIR_SCAN_THREADS asks
     threads = int(os.environ.get("CIR_SCAN_THREADS", "0"))
@@ -703,6 +758,27 @@ def run_config5(args, ca, ctx, ctx_init_s=None):
     cfg = ca.ScannerConfig.new().threads(threads).add_dir(args.tree_dir, "/")
     if sha:
         cfg.hash(ca.HashType.sha512_256())
+    # the cold scan: the library's scan of the tree this process has just
+    # written, before anything else has read it -- what `ciruela sync` right
+    # after the tree was written sees (the first read of fresh tmpfs pages
+    # bounds it, not PCIe: tree_first_read below)
+    cold = None
+    if fresh:
+        ctx.scan_timing(True)
+        t0 = time.perf_counter()
+        got = bytearray()
+        ca.v1.scan(cfg, out=got, context=ctx)
+        dt = time.perf_counter() - t0
+        summ = scan_batch_summary(ctx.scan_batches(), ctx.scan_phases())
+        ctx.scan_timing(False)
+        cold = {"seconds": round(dt, 4), "value": round(nbytes / dt / GIB, 3),
+                "index": bytes(got),
+                "read_gbs_median": (summ or {}).get("read_gbs_median"),
+                "copy_busy_frac": (summ or {}).get("copy_busy_frac"),
+                "h2d_ms_median": (summ or {}).get("h2d_ms", {}).get("median")}
+        del got
+    rd_bytes, rd_s = tree_read_pass(args.tree_dir)
+    rd2_bytes, rd2_s = tree_read_pass(args.tree_dir)
     # footer placement: the library default (host), the GPU chain, or both
     # alternating in one process (--footer ab); every scan is timed per batch
     modes = {"host": ["host"], "gpu": ["gpu"], "ab": ["host", "gpu"]}[args.footer]
@@ -776,11 +852,20 @@ def run_config5(args, ca, ctx, ctx_init_s=None):
                              sum(len(os.listdir(d)) for d in sample), sample_bytes / GIB))
     cpu["full_tree"] = {"seconds": round(full_s, 3), "cores": per_gpu_share(),
                         "value": round(nbytes / full_s / GIB, 4)}
+    if cold is not None:
+        cold_index = cold.pop("index")
+        cold["matches_oracle"] = cold_index == want
+        cold["note"] = ("one scan of the tree right after this process wrote it, before any "
+                        "read pass: bounded by the first read of fresh tmpfs pages "
+                        "(tree_first_read), not by PCIe")
+    else:
+        cold = {"skipped": "the tree was left by an earlier run (not freshly written)"}
     return {"metric": "GiB/s end-to-end index of a tmpfs tree (config 5)",
             "value": round(nbytes / best / GIB, 3), "unit": "GiB/s",
             "seconds_best": round(best, 3), "seconds_all": [round(t, 3) for t in times],
             "seconds_first": round(times[0], 3),
             "value_first": round(nbytes / times[0] / GIB, 3),
+            "value_cold": cold.get("value"), "cold_scan": cold,
             "context_init_s": round(ctx_init_s, 3) if ctx_init_s is not None else None,
             "config": {"workload": "config5: %d files x 32 MiB in 40 dirs (%.0f GiB) on tmpfs, "
                                    "%s (reads -> pinned -> H2D -> hash -> D2H; footer "
@@ -809,15 +894,17 @@ def run_config5(args, ca, ctx, ctx_init_s=None):
                        "copy_busy_frac": (sc["batches"] or {}).get("copy_busy_frac")}
                       for sc in scans],
             "files": nfiles, "bytes": nbytes, "index_bytes": len(index),
-            "image_id": ca.get_hash(index).hex(), "matches_oracle": index == want,
+            "image_id": ca.get_hash(index).hex(),
+            "matches_oracle": index == want and cold.get("matches_oracle", True),
             "tree_gen_s": round(gen_s, 1),
             "reader_threads": threads or "auto (min(12, 3/4 of the CPU share))",
             "tree": args.tree_dir,
             "tree_first_read": {"seconds": round(rd_s, 3), "value": round(rd_bytes / rd_s / GIB, 2),
                                 "second_pass_value": round(rd2_bytes / rd2_s / GIB, 2),
-                                "note": "plain 16-thread CPU read of the tree before the scans "
-                                        "(no GPU): the first read of freshly written tmpfs "
-                                        "pages, then a second pass"},
+                                "note": "plain 16-thread CPU read of the tree before the timed "
+                                        "scans (no GPU): the first read after the cold scan "
+                                        "(or of freshly written pages when there was none), "
+                                        "then a second pass"},
             "cpu_baseline": cpu}
 
 
@@ -838,19 +925,47 @@ def make_config1_tree(root):
     return int(sizes.sum())
 
 
+CONFIG1_ROOT = "/tmp/ciruela_cfg1_tree"
+
+
+def time_cli_config1(runs=6):
+    """`ciruela-index sync --append` of the config-1 tree as separate
+    processes, timed from the parent's side (fork + exec + HIP start-up +
+    scan + exit).  bench.py calls it before it touches a GPU itself (no
+    torch.cuda call, no context yet), so each CLI process has the GPU to
+    itself: the first run and the median of all `runs`."""
+    import subprocess
+    make_config1_tree(CONFIG1_ROOT)
+    cli = os.path.join(ROOT, "bin", "ciruela-index")
+    times, out = [], None
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        out = subprocess.check_output([cli, "sync", "--append", CONFIG1_ROOT + ":/bench"])
+        times.append(time.perf_counter() - t0)
+    return {"seconds_first": round(times[0], 4),
+            "seconds_median": round(sorted(times)[len(times) // 2], 4),
+            "seconds_all": [round(t, 4) for t in times], "runs": runs,
+            "image_id": out.decode().split()[0]}
+
+
 def run_config1(args, ca, ctx):
     """100 files / 10 MiB, 10 subdirectories, through the `ciruela-index sync`
     CLI (the indexing half of `ciruela sync --append`, one process: HIP
     start-up included) and through v1::scan in this process (warm), checked
     against the scan oracle; CPU baseline = the CPU indexer restatement on
-    the same tree."""
+    the same tree.  The CLI figures are those main() took before this
+    process touched the GPU (args.cli_pre), plus one run now, beside this
+    process's own context, for comparison."""
     import subprocess
-    root = "/tmp/ciruela_cfg1_tree"
+    root = CONFIG1_ROOT
     total = make_config1_tree(root)
     cli = os.path.join(ROOT, "bin", "ciruela-index")
+    pre = getattr(args, "cli_pre", None)
     t0 = time.perf_counter()
     out = subprocess.check_output([cli, "sync", "--append", root + ":/bench"])
     cli_s = time.perf_counter() - t0
+    if isinstance(pre, dict) and "image_id" in pre and pre["image_id"] != out.decode().split()[0]:
+        raise SystemExit("config1: the CLI's image id changed between runs")
     cfg = ca.ScannerConfig.new().add_dir(root, "/")  # threads(4), the reference default
     warm = []
     for _ in range(max(3, args.steps)):
@@ -872,14 +987,21 @@ def run_config1(args, ca, ctx):
             "value": round(total / best / GIB, 4), "unit": "GiB/s",
             "seconds_best": round(best, 5), "seconds_all": [round(t, 5) for t in warm],
             "config": {"workload": "config1: 100 files, %d bytes, 10 subdirectories" % total},
-            "cli_seconds": round(cli_s, 3), "oracle_python_seconds": round(oracle_s, 3),
+            "cli_seconds": (pre or {}).get("seconds_median", round(cli_s, 3)),
+            "cli_seconds_first": (pre or {}).get("seconds_first"),
+            "cli": pre if pre else {"skipped": "not measured before the bench's context"},
+            "cli_seconds_beside_bench_context": round(cli_s, 3),
+            "oracle_python_seconds": round(oracle_s, 3),
             "image_id": image_id,
             "matches_oracle": want.endswith(image_id.encode() + b"\n") and index == want,
             "cpu_baseline": cpu_record(rates, "the whole config-1 tree indexed by "
                                        "oracle/cpu_indexer.py (file-level pool, C BLAKE2b), "
                                        "repeated; 4 threads = reference default --disk-threads"),
-            "note": "value = in-process v1::scan (warm context, threads 4); cli_seconds is one "
-                    "`ciruela-index sync` process including HIP start-up"}
+            "note": "value = in-process v1::scan (warm context, threads 4); cli_seconds = the "
+                    "median of `cli.runs` `ciruela-index sync` processes (HIP start-up and exit "
+                    "included) timed before this process touched the GPU, cli_seconds_first the "
+                    "first of them; cli_seconds_beside_bench_context = one more while this "
+                    "process holds its context and torch's allocator on the same GPU"}
 
 
 def mem_available_gib():
@@ -920,6 +1042,7 @@ def run_config5_leg(args, ca, ctx, dev, stream):
         if avail is not None and avail < need + 8:
             return {"skipped": "MemAvailable %.1f GiB, the %.0f GiB tmpfs tree needs %.0f + 8"
                                % (avail, args.tree_gib, need), "matches_oracle": None}
+    args.tree_fresh = not tree_complete(args.tree_dir, args.tree_gib)
     try:
         try:
             make_tree(args.tree_dir, args.tree_gib)
@@ -1023,6 +1146,16 @@ def dry_run(args, rank, world):
         dist.all_gather(parts, bounds)
     else:
         parts = [bounds]
+    # no GPU here: each rank stands in its host and pid for a device (one
+    # shared stand-in with --dry-run-shared-device); the rule is the one the
+    # real run applies for --dist-backend
+    import socket
+    ident = {"pci_bus_id": "dry-run-shared" if args.dry_run_shared_device else
+             "dry-run:%s:%d" % (socket.gethostname(), os.getpid()), "uuid": None}
+    devices = gather_objects(ident)
+    distinct, problem = devices_check(devices, args.dist_backend == "nccl")
+    if problem and problem.startswith("FAIL"):
+        parity = problem if parity == "ok" else parity + "; " + problem
     if rank == 0:
         print(json.dumps({
             "dry_run": True, "metric": METRIC, "n_gpus": world,
@@ -1033,6 +1166,8 @@ def dry_run(args, rank, world):
             "parity": parity, "parity_checked_blocks": checked_all,
             "per_rank": [{"rank": i, "mismatches": int(r[0]), "checked": int(r[1]),
                           "kernel_ms_avg": r[3]} for i, r in enumerate(rows)],
+            "devices_seen": [dict(d, rank=i) for i, d in enumerate(devices)],
+            "devices_distinct": distinct, "devices_note": problem,
             "shards": [p.tolist() for p in parts]}), flush=True)
     if distributed:
         dist.destroy_process_group()
@@ -1053,6 +1188,15 @@ def main():
         log("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
     if args.dry_run:
         return dry_run(args, rank, world)
+    # config 1's one-shot CLI, timed while no process of this job holds the
+    # GPU (this process has made no GPU call yet and opens no context until
+    # after it)
+    if world == 1 and not args.force_dist and (
+            args.workload == "config1" or (args.workload == "auto" and not args.no_secondary)):
+        try:
+            args.cli_pre = time_cli_config1()
+        except Exception as e:  # noqa: BLE001 - reported in the config-1 record
+            args.cli_pre = {"error": "%s: %s" % (type(e).__name__, e)}
     import torch
     import torch.distributed as dist
 
@@ -1181,6 +1325,13 @@ def main():
     rows = job_summary([nbad, checked, failed, sum(kern_ms) / len(kern_ms), min(kern_ms)],
                        coll_dev)
     parity, checked_all = job_parity(rows, "; ".join(reasons) if rank == 0 else None)
+    # which GPU each rank ran on, as its driver and its own clocks see it
+    devices = distinct = devices_problem = None
+    if distributed:
+        devices = gather_objects(device_identity(ca, local % ndev))
+        distinct, devices_problem = devices_check(devices, args.dist_backend == "nccl")
+        if devices_problem and devices_problem.startswith("FAIL"):
+            parity = devices_problem if parity == "ok" else parity + "; " + devices_problem
     valu_ms = valu_ceiling(ca, nblk, bs, stream)
 
     if rank == 0:
@@ -1250,6 +1401,9 @@ def main():
             # the process group's own count: every rank of the job took part
             rec["ranks_seen"] = dist.get_world_size()
             rec["dist_backend"] = args.dist_backend
+            rec["devices_seen"] = [dict(d, rank=i) for i, d in enumerate(devices)]
+            rec["devices_distinct"] = distinct
+            rec["devices_note"] = devices_problem
         if ranks_per_gpu > 1:
             rec["config"]["ranks_per_gpu"] = ranks_per_gpu
         if not distributed and not args.no_cpu_baseline:

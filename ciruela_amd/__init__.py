@@ -288,8 +288,10 @@ class Context:
                          "footer_feeds")
 
     def set_footer_mode(self, mode):
-        """Where cir_scan_v1 hashes a blake2b/256 footer: FOOTER_HOST (one host
-        thread beside the scan, the default) or FOOTER_GPU (the chain kernel)."""
+        """Where cir_scan_v1 and cir_index_rewrite hash an index's footer, in
+        either hash type: FOOTER_HOST (a host thread, the default) or
+        FOOTER_GPU (blake2b/256: the chain kernel beside the scan;
+        sha512/256: one lane at the end)."""
         _n.check(_n.lib.cir_set_footer_mode(self._h, mode))
 
     def scan_timing(self, enable=True):

@@ -117,6 +117,8 @@ _SIGS = {
                                       ctypes.c_size_t, ctypes.POINTER(ctypes.c_int)]),
     "cir_debug_compress_only_dev": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, c_vp, c_vp]),
     "cir_debug_relay_blocks": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint64]),
+    "cir_debug_device_identity": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t,
+                                                 c_vp, ctypes.POINTER(ctypes.c_uint64)]),
     "cir_debug_desc_timing": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "cir_debug_desc_times": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double)]),
     "cir_verify_submit": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, ctypes.c_size_t, c_vp,

@@ -94,6 +94,15 @@ static uint64_t staging_for(uint64_t total) {
   return std::max<uint64_t>(kMin, (total + kMin - 1) / kMin * kMin);
 }
 
+// A profiling tool library loaded into this process (rocprofv3's
+// environment), which writes its output from the exit handlers.
+static bool profiled() {
+  extern char** environ;
+  for (char** e = environ; e && *e; ++e)
+    if (!strncmp(*e, "ROCP_TOOL_LIBRARIES=", 20) || !strncmp(*e, "ROCPROF", 7)) return true;
+  return false;
+}
+
 struct Job {
   std::string kind, src, dest;
 };
@@ -254,12 +263,19 @@ int main(int argc, char** argv) {
   // teardown -- freeing the pinned staging, streams and device buffers one by
   // one, ~17 ms of a ~0.2 s run (profiles/r04/cli_startup.log) -- is left to
   // process exit, as the error paths above already do.  CIR_CLI_TEARDOWN=1
-  // destroys the context first (leak checks).
+  // destroys the context first (leak checks).  Under a profiler (rocprofv3
+  // sets ROCP_TOOL_LIBRARIES / ROCPROF_* for its tool library) the process
+  // still skips cir_destroy but returns normally, so the exit handlers run
+  // and the tool writes its trace at finalisation.
   const char* td = getenv("CIR_CLI_TEARDOWN");
   if (!(td && *td && strcmp(td, "0") != 0)) {
     if (fflush(stdout) != 0) {
       perror("stdout");
       return 1;
+    }
+    if (profiled()) {
+      if (trace) fprintf(stderr, "ciruela-index: profiler present: normal exit, no cir_destroy\n");
+      return 0;
     }
     if (trace) fprintf(stderr, "ciruela-index: exit without cir_destroy\n");
     fflush(stderr);

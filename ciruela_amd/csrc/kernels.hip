@@ -1569,6 +1569,26 @@ hipError_t launch_mixed(const uint8_t* arena, const uint64_t* off, const uint32_
   return e;
 }
 
+// The device's own clocks, read by one wave: the constant-rate wall clock
+// (s_memrealtime) and the shader clock counter (s_memtime) before and after
+// a spin of `spin` wall-clock ticks (bounded by an iteration cap, so the wave
+// always ends).  Lanes 0-3 store rt0, rt1, c0, c1 with per-lane addresses.
+__global__ void k_clock_probe(uint64_t* __restrict__ out, uint64_t spin) {
+  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+  const uint64_t c0 = __builtin_amdgcn_s_memtime();
+  uint64_t rt1 = rt0;
+  for (uint32_t it = 0; it < (1u << 22) && rt1 - rt0 < spin; ++it)
+    rt1 = __builtin_amdgcn_s_memrealtime();
+  const uint64_t c1 = __builtin_amdgcn_s_memtime();
+  const unsigned l = threadIdx.x;
+  if (l < 4) out[l] = l == 0 ? rt0 : l == 1 ? rt1 : l == 2 ? c0 : c1;
+}
+
+hipError_t launch_clock_probe(uint64_t* out, uint64_t spin, hipStream_t s) {
+  hipLaunchKernelGGL(k_clock_probe, dim3(1), dim3(64), 0, s, out, spin);
+  return hipGetLastError();
+}
+
 hipError_t launch_fill_splitmix64(uint64_t* p, uint64_t nwords, uint64_t seed,
                                   uint64_t block_words, uint64_t first_block, hipStream_t s) {
   if (nwords == 0) return hipSuccess;

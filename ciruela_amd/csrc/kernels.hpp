@@ -130,6 +130,9 @@ hipError_t launch_verify(const uint8_t* got, const uint8_t* want, uint64_t n, ui
 // nlanes x `lines` register-only compressions (diagnostic VALU ceiling).
 hipError_t launch_compress_only(uint64_t nlanes, uint32_t lines, uint8_t* out, hipStream_t s);
 
+// one wave reads the device's wall clock and shader clock counters around a
+// spin of `spin` wall-clock ticks: out[0..3] = rt0, rt1, c0, c1 (device memory)
+hipError_t launch_clock_probe(uint64_t* out, uint64_t spin, hipStream_t s);
 hipError_t launch_fill_splitmix64(uint64_t* p, uint64_t nwords, uint64_t seed,
                                   uint64_t block_words, uint64_t first_block, hipStream_t s);
 

@@ -1743,6 +1743,32 @@ int cir_debug_desc_times(cir_ctx* ctx, double out[5]) {
   return CIR_OK;
 }
 
+int cir_debug_device_identity(int device, char* pci_bus_id, size_t len, uint8_t uuid[16],
+                              uint64_t clocks[5]) {
+  if (!pci_bus_id || len < 13 || !uuid || !clocks) return fail(CIR_EINVAL, "null pointer");
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
+    return fail(CIR_ENODEV, "no such HIP device");
+  DeviceGuard guard;
+  CIR_HIP(hipSetDevice(device));
+  CIR_HIP(hipDeviceGetPCIBusId(pci_bus_id, (int)std::min<size_t>(len, 256), device));
+  hipUUID u;
+  CIR_HIP(hipDeviceGetUuid(&u, device));
+  memcpy(uuid, u.bytes, 16);
+  int rate_khz = 0;
+  CIR_HIP(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, device));
+  uint64_t* d = nullptr;
+  CIR_HIP(hipMalloc(&d, 4 * sizeof(uint64_t)));
+  // ~100 us of wall-clock ticks between the two reads
+  const uint64_t spin = std::max<uint64_t>(1, (uint64_t)rate_khz / 10);
+  hipError_t e = dev::launch_clock_probe(d, spin, nullptr);
+  if (e == hipSuccess) e = hipMemcpy(clocks, d, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return hip_fail(e, "clock probe");
+  clocks[4] = (uint64_t)rate_khz;
+  return CIR_OK;
+}
+
 uint64_t cir_debug_relay_blocks(uint64_t nfull, uint64_t block_size) {
   return dev::relay_blocks(nfull, block_size);
 }

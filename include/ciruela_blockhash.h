@@ -278,9 +278,10 @@ int cir_index_get_hash(const uint8_t* index, size_t len, uint8_t* id_out, size_t
 /* RawIndex::into_mut + MutableIndex::to_raw_data (src/cluster/download.rs:
  * 171-188, 266-319): parse, rebuild the directory tree and re-emit it in the
  * reference's order (files and links by name, then subdirectories; empty
- * directories dropped) with the footer recomputed -- with the index's hash
- * type: a blake2b/256 footer where cir_set_footer_mode says (a host thread
- * by default, as in cir_scan_v1), a sha512/256 footer on the GPU. */
+ * directories dropped) with the footer recomputed in the index's hash type
+ * where cir_set_footer_mode says: CIR_FOOTER_HOST (the default, as in
+ * cir_scan_v1) hashes it on the calling thread, blake2b/256 and sha512/256
+ * alike; CIR_FOOTER_GPU as one descriptor on the GPU. */
 int cir_index_rewrite(cir_ctx* ctx, const uint8_t* in, size_t len, uint8_t** out, size_t* out_len);
 
 /* ---- consumers of the index (host bookkeeping) ------------------------ */
@@ -385,6 +386,16 @@ int cir_debug_host_blake2b256(const uint8_t* p, size_t n, size_t piece,
                               uint8_t out[CIR_DIGEST_BYTES]);
 int cir_debug_host_sha512_256(const uint8_t* p, size_t n, size_t piece,
                               uint8_t out[CIR_DIGEST_BYTES]);
+
+/* Identity of HIP device `device` as its driver and its own counters see it
+ * (the multi-GPU bench puts every rank's into its line): the PCI bus id
+ * (hipDeviceGetPCIBusId, into pci_bus_id, len >= 13), the UUID
+ * (hipDeviceGetUuid), and one wave's reads of the device's wall clock and
+ * shader clock counters ~100 us apart: clocks[0], [1] = wall clock before /
+ * after, [2], [3] = shader clock counter before / after, [4] = the wall
+ * clock's rate in kHz.  Synchronous; allocates and frees 32 bytes. */
+int cir_debug_device_identity(int device, char* pci_bus_id, size_t len, uint8_t uuid[16],
+                              uint64_t clocks[5]);
 
 /* How many whole blocks of a file of nfull x block_size bytes (plus any short
  * last block) cir_hash_chunks_dev with a context relays on the calling

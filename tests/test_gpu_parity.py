@@ -1884,14 +1884,14 @@ def test_verify_async_blocks_share_batches(gpu, oracle):
     c.close()
 
 
-def _blocks_with_bad(oracle, rng, n, size=32768, every=5):
-    """n random blocks, their oracle digests, one in `every` expected digest
-    corrupted: [(data, expected, good)]."""
+def _blocks_with_bad(oracle, rng, n, size=32768, every=5, bad=2):
+    """n random blocks, their oracle digests, the expected digest of every
+    block i with i % every == bad corrupted: [(data, expected, good)]."""
     out = []
     for i in range(n):
         data = rng.randbytes(size)
         want = oracle_digest(oracle, data)
-        good = i % every != 2
+        good = i % every != bad
         out.append((data, want if good else bytes([want[0] ^ 0x40]) + want[1:], good))
     return out
 
@@ -1910,7 +1910,7 @@ def test_verify_async_queue_is_bounded(gpu, oracle):
     # non-blocking: 64 KiB bound, 40 KiB blocks, a 100 ms window
     c.verify_limits(max_bytes=64 << 10, nonblocking=True)
     c.verify_window(100000)
-    a, b = _blocks_with_bad(oracle, rng, 2, size=40 << 10, every=2)  # b's digest is wrong
+    a, b = _blocks_with_bad(oracle, rng, 2, size=40 << 10, every=2, bad=1)  # b's digest is wrong
     ta = c.verify_submit(a[0], a[1])
     with pytest.raises(n.CiruelaError) as e:
         c.verify_submit(b[0], b[1])

@@ -180,3 +180,40 @@ def test_force_dist_launches_one_rank():
     rec = _line(r)
     assert rec["ranks_seen"] == 1 and rec["config"]["workload"] == "config4"
     assert rec["parity"] == "ok"
+
+
+def test_devices_seen_in_the_line():
+    """The N>1 line carries every rank's device identity (devices_seen,
+    gathered over the process group) and whether they are distinct.  Under
+    --dist-backend nccl (one GPU per rank) two ranks on one device fail the
+    line and the job; a gloo rehearsal with shared GPUs only notes it."""
+    r = _run_bench(["--gpus", "2", "--dist-backend", "gloo", "--dry-run", "--steps", "1",
+                    "--blocks", "16"])
+    rec = _line(r)
+    assert r.returncode == 0 and rec["devices_distinct"] is True
+    assert [d["rank"] for d in rec["devices_seen"]] == [0, 1]
+    assert len({d["pci_bus_id"] for d in rec["devices_seen"]}) == 2
+    r = _run_bench(["--gpus", "2", "--dist-backend", "nccl", "--dry-run", "--steps", "1",
+                    "--blocks", "16", "--dry-run-shared-device"])
+    rec = _line(r)
+    assert r.returncode != 0 and rec["devices_distinct"] is False
+    assert rec["parity"].startswith("FAIL") and "share a device" in rec["parity"]
+    r = _run_bench(["--gpus", "2", "--dist-backend", "gloo", "--dry-run", "--steps", "1",
+                    "--blocks", "16", "--dry-run-shared-device"])
+    rec = _line(r)
+    assert r.returncode == 0 and rec["parity"] == "ok" and rec["devices_distinct"] is False
+    assert "share a device" in rec["devices_note"]
+
+
+def test_devices_check_rule():
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    a = {"pci_bus_id": "0000:05:00.0", "uuid": "aa"}
+    b = {"pci_bus_id": "0000:15:00.0", "uuid": "bb"}
+    assert bench.devices_check([a, b], True) == (True, None)
+    ok, msg = bench.devices_check([a, b, dict(a)], True)
+    assert not ok and msg.startswith("FAIL") and "0/2" in msg
+    ok, msg = bench.devices_check([a, {"pci_bus_id": "0000:99:00.0", "uuid": "aa"}], False)
+    assert not ok and not msg.startswith("FAIL")  # same UUID, another bus id: still one device
+    assert bench.devices_check([a], True) == (True, None)
