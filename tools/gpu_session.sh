@@ -24,8 +24,6 @@ step() {  # name timeout cmd...
 
 for s in "$@"; do
   case "$s" in
-    diag)
-      step diag 400 python -X faulthandler tools/diag.py ;;
     ablib)
       step ablib 600 python tools/ab_lib.py abtest/*.so > gpurun_out/ablib.log 2>&1
       cat gpurun_out/ablib.log ;;
@@ -37,28 +35,11 @@ for s in "$@"; do
       step abquadtrace 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/abqt \
         -o run -- python3 tools/ab_quad.py "$lib" > gpurun_out/abquadtrace.log 2>&1
       cat gpurun_out/abquadtrace.log | grep -v amdgpu.ids ;;
-    h2d)
-      step h2d 300 python tools/h2d_probe.py > gpurun_out/h2d.log 2>&1
-      HSA_ENABLE_SDMA=0 step h2d_blit 300 python tools/h2d_probe.py > gpurun_out/h2d_blit.log 2>&1
-      cat gpurun_out/h2d.log gpurun_out/h2d_blit.log ;;
     cfg5blit)
       HSA_ENABLE_SDMA=0 step cfg5blit 1000 python bench.py --workload config5 --steps 3 \
         --tree-gib "${TREE_GIB:-50}" > gpurun_out/cfg5blit.json 2> gpurun_out/cfg5blit.err
       rm -rf /dev/shm/ciruela_bench_tree
       cat gpurun_out/cfg5blit.json ;;
-    batch)
-      step batch 300 python tools/batch_probe.py > gpurun_out/batch.log 2>&1
-      cat gpurun_out/batch.log ;;
-    hostreg)
-      step hostreg 300 python tools/hostreg_probe.py > gpurun_out/hostreg.log 2>&1
-      rm -f /dev/shm/hostreg_probe.bin
-      cat gpurun_out/hostreg.log ;;
-    hostreg2)
-      step hostreg2 300 python tools/hostreg_probe2.py > gpurun_out/hostreg2.log 2>&1
-      rm -rf /dev/shm/hostreg2
-      cat gpurun_out/hostreg2.log ;;
-    shadiag)
-      step shadiag 300 python tools/sha_diag.py ;;
     cli)
       head -c 100000 /dev/urandom > /tmp/cli_probe.bin
       step cli 120 ./bin/ciruela-index hash /tmp/cli_probe.bin ;;
