@@ -21,9 +21,7 @@
 #include <cstdlib>
 #include <deque>
 #include <thread>
-#include <map>
 #include <unordered_map>
-#include <unordered_set>
 
 namespace cir {
 
@@ -1398,142 +1396,22 @@ int cir_verify_blocks(cir_ctx* ctx, int hash_type, const uint8_t* h_arena, const
 }  // extern "C"
 
 // ---- asynchronous verify (row f2, the daemon's per-block caller) --------
-// FetchBlock::poll hashes each received block as it arrives
-// (src/daemon/tracking/fetch_blocks.rs:77).  cir_verify_submit packs one
-// block (one copy) into the arena of the batch being formed for its hash
-// type and returns at once; a worker thread per context takes the oldest
-// batch once it is full (av_max_batch blocks, or its arena) or av_window_us
-// after its first block, and verifies it as one host batch
-// (cir_hash_blocks_ht, straight from that arena); callers poll or wait for
-// their ticket.  One batch costs about one chain's latency whatever its size
-// below a few thousand blocks, so blocks that arrive
-// together share it.
-//
-// Bounds (cir_verify_limits): the block bytes accepted and not yet verified
-// stay within max_bytes -- a submit that would pass it waits for the worker
-// (or, non-blocking, returns CIR_EAGAIN: the daemon's backpressure); at most
-// max_results finished outcomes are held for their tickets, the oldest
-// dropped beyond that; cir_verify_forget drops a ticket the caller no longer
-// wants (the reference retries such a block elsewhere, :91-103).
+// The queue, its worker and its bounds are verify_queue.hpp; a context's
+// queue hashes each batch as one host batch straight from the batch's arena
+// (cir_hash_blocks_ht), created on the first verify call.
 namespace cir {
 
-constexpr uint64_t kVerifyMaxBytes = 256ull << 20;  // two batches of 4096 x 32 KiB
-constexpr uint64_t kVerifyMaxResults = 1ull << 20;
-
-struct AsyncVerify {
-  // a batch being formed or waiting for the worker: its blocks packed into
-  // one arena as they were submitted
-  struct Batch {
-    int ht = 0;
-    std::vector<uint8_t> arena;  // reserved once: appends never move it
-    std::vector<uint64_t> off;
-    std::vector<uint32_t> len;
-    std::vector<uint8_t> expected;
-    std::vector<uint64_t> tickets;
-    std::chrono::steady_clock::time_point first;
-    bool sealed = false;  // full: the worker takes it without waiting
-  };
-  cir_ctx* ctx = nullptr;
-  std::mutex mu;
-  std::condition_variable cv, done_cv, room_cv;
-  std::deque<std::unique_ptr<Batch>> queue;
-  std::unordered_set<uint64_t> pending;  // submitted, outcome not yet known
-  std::map<uint64_t, int> done;          // outcome held: 1 match, 2 mismatch, < 0 error
-  std::unordered_map<uint64_t, std::string> errors;
-  uint64_t next_ticket = 1;
-  uint64_t held = 0, peak = 0;  // block bytes accepted and not yet verified
-  uint64_t max_bytes = kVerifyMaxBytes, max_results = kVerifyMaxResults;
-  bool nonblocking = false;
-  uint64_t expired = 0, forgotten = 0, refused = 0, batches = 0;
-  bool stop = false;
-  std::thread worker;
-
-  // arena bytes of one batch: half the byte bound, so one batch can form
-  // while the previous one is verified
-  uint64_t batch_bytes() const { return std::max<uint64_t>(1, max_bytes / 2); }
-
-  void evict() {
-    while (done.size() > max_results) {
-      errors.erase(done.begin()->first);
-      done.erase(done.begin());
-      ++expired;
-    }
-  }
-
-  void run() {
-    std::unique_lock<std::mutex> lk(mu);
-    for (;;) {
-      cv.wait(lk, [&] { return stop || !queue.empty(); });
-      if (queue.empty()) return;  // stopped and drained
-      Batch* b = queue.front().get();
-      const auto deadline = b->first + std::chrono::microseconds(ctx->av_window_us);
-      cv.wait_until(lk, deadline, [&] { return stop || b->sealed; });
-      std::unique_ptr<Batch> bp = std::move(queue.front());
-      queue.pop_front();
-      bp->sealed = true;  // (no more appends)
-      lk.unlock();
-      const size_t n = bp->tickets.size();
-      std::vector<uint8_t> got(32 * n);
-      static const uint8_t empty = 0;
-      const int rc = cir_hash_blocks_ht(ctx, bp->ht, bp->arena.empty() ? &empty : bp->arena.data(),
-                                        bp->off.data(), bp->len.data(), n, got.data());
-      const std::string err = rc ? cir_last_error() : std::string();
-      const uint64_t bytes = bp->arena.size();
-      lk.lock();
-      for (size_t i = 0; i < n; ++i) {
-        const uint64_t t = bp->tickets[i];
-        if (!pending.erase(t)) continue;  // forgotten meanwhile: no outcome held
-        if (rc) {
-          done[t] = rc;
-          errors[t] = err;
-        } else {
-          done[t] = memcmp(got.data() + 32 * i, bp->expected.data() + 32 * i, 32) == 0 ? 1 : 2;
-        }
-      }
-      held -= bytes;
-      ++batches;
-      evict();
-      room_cv.notify_all();
-      done_cv.notify_all();
-      lk.unlock();
-      bp.reset();  // the arena is freed outside the lock
-      lk.lock();
-    }
-  }
-};
-
-void AsyncVerifyDeleter::operator()(AsyncVerify* p) const {
-  {
-    std::lock_guard<std::mutex> lk(p->mu);
-    p->stop = true;
-  }
-  p->cv.notify_all();
-  if (p->worker.joinable()) p->worker.join();
-  delete p;
-}
-
-static AsyncVerify* async_verify(cir_ctx* ctx) {
+static VerifyQueue* verify_queue(cir_ctx* ctx) {
   std::lock_guard<std::mutex> lk(ctx->av_mu);
-  if (!ctx->av) {
-    AsyncVerify* a = new AsyncVerify;
-    a->ctx = ctx;
-    ctx->av.reset(a);
-    a->worker = std::thread([a] { a->run(); });
-  }
+  if (!ctx->av)
+    ctx->av = std::make_unique<VerifyQueue>(
+        [ctx](int ht, const uint8_t* arena, const uint64_t* off, const uint32_t* len, size_t n,
+              uint8_t* out, std::string* err) {
+          const int rc = cir_hash_blocks_ht(ctx, ht, arena, off, len, n, out);
+          if (rc) *err = cir_last_error();
+          return rc;
+        });
   return ctx->av.get();
-}
-
-// A held outcome, consumed: 1 match, 2 mismatch, < 0 error.
-static int take_result(AsyncVerify& a, std::map<uint64_t, int>::iterator it) {
-  const uint64_t ticket = it->first;
-  const int r = it->second;
-  a.done.erase(it);
-  if (r < 0) {
-    const std::string e = a.errors[ticket];
-    a.errors.erase(ticket);
-    return fail(r, e);
-  }
-  return r;
 }
 
 }  // namespace cir
@@ -1545,137 +1423,52 @@ int cir_verify_submit(cir_ctx* ctx, int hash_type, const uint8_t* data, size_t n
   if (!ctx || !ticket || !expected || (n && !data)) return fail(CIR_EINVAL, "null pointer");
   if (!valid_hash_type(hash_type)) return fail(CIR_EINVAL, "unknown hash type");
   if (n > 0xffffffffull) return fail(CIR_EINVAL, "block longer than 4 GiB");
-  AsyncVerify* a = async_verify(ctx);
-  std::unique_lock<std::mutex> lk(a->mu);
-  // room: a block always fits an empty queue, whatever its size
-  while (a->held && a->held + n > a->max_bytes) {
-    if (a->nonblocking) {
-      ++a->refused;
-      return fail(CIR_EAGAIN, "verify queue full (" + std::to_string(a->held) + " of " +
-                                  std::to_string(a->max_bytes) + " bytes held)");
-    }
-    a->room_cv.wait(lk);
-  }
-  AsyncVerify::Batch* b = nullptr;
-  for (auto it = a->queue.rbegin(); it != a->queue.rend(); ++it)
-    if (!(*it)->sealed && (*it)->ht == hash_type) {
-      b = it->get();
-      break;
-    }
-  if (b && b->arena.size() + n > b->arena.capacity()) {
-    b->sealed = true;  // full: this block opens the next batch
-    b = nullptr;
-  }
-  if (!b) {
-    auto nb = std::make_unique<AsyncVerify::Batch>();
-    nb->ht = hash_type;
-    nb->arena.reserve(std::max<uint64_t>(n, a->batch_bytes()));
-    nb->first = std::chrono::steady_clock::now();
-    b = nb.get();
-    a->queue.push_back(std::move(nb));
-  }
-  b->off.push_back(b->arena.size());
-  b->len.push_back((uint32_t)n);
-  b->arena.insert(b->arena.end(), data, data + n);
-  b->expected.insert(b->expected.end(), expected, expected + 32);
-  const uint64_t t = a->next_ticket++;
-  b->tickets.push_back(t);
-  if (b->tickets.size() >= ctx->av_max_batch) b->sealed = true;
-  a->pending.insert(t);
-  a->held += n;
-  a->peak = std::max(a->peak, a->held);
-  *ticket = t;
-  lk.unlock();
-  a->cv.notify_one();
-  return CIR_OK;
+  std::string err;
+  const int rc = verify_queue(ctx)->submit(hash_type, data, n, expected, ticket, &err);
+  return rc ? fail(rc, err) : CIR_OK;
 }
 
 int cir_verify_poll(cir_ctx* ctx, uint64_t ticket, int* state) {
   if (!ctx || !state) return fail(CIR_EINVAL, "null pointer");
-  AsyncVerify* a = async_verify(ctx);
-  std::lock_guard<std::mutex> lk(a->mu);
-  if (a->pending.count(ticket)) {
-    *state = 0;
-    return CIR_OK;
-  }
-  auto r = a->done.find(ticket);
-  if (r == a->done.end())
-    return fail(CIR_ENOTFOUND, "unknown, consumed, forgotten or expired ticket");
-  const int v = take_result(*a, r);
-  if (v < 0) return v;
+  std::string err;
+  const int v = verify_queue(ctx)->poll(ticket, &err);
+  if (v < 0) return fail(v, err);
   *state = v;
   return CIR_OK;
 }
 
 int cir_verify_wait(cir_ctx* ctx, uint64_t ticket, int* ok) {
   if (!ctx || !ok) return fail(CIR_EINVAL, "null pointer");
-  AsyncVerify* a = async_verify(ctx);
-  std::unique_lock<std::mutex> lk(a->mu);
-  if (!a->pending.count(ticket) && !a->done.count(ticket))
-    return fail(CIR_ENOTFOUND, "unknown, consumed, forgotten or expired ticket");
-  a->done_cv.wait(lk, [&] { return !a->pending.count(ticket); });
-  // (consumed by another caller's poll, forgotten or expired meanwhile)
-  auto r = a->done.find(ticket);
-  if (r == a->done.end())
-    return fail(CIR_ENOTFOUND, "ticket consumed, forgotten or expired while waiting");
-  const int v = take_result(*a, r);
-  if (v < 0) return v;
+  std::string err;
+  const int v = verify_queue(ctx)->wait(ticket, &err);
+  if (v < 0) return fail(v, err);
   *ok = v == 1;
   return CIR_OK;
 }
 
 int cir_verify_forget(cir_ctx* ctx, uint64_t ticket) {
   if (!ctx) return fail(CIR_EINVAL, "null ctx");
-  AsyncVerify* a = async_verify(ctx);
-  std::lock_guard<std::mutex> lk(a->mu);
-  if (a->pending.erase(ticket)) {
-    // still queued or in flight: its bytes are released with its batch and
-    // its outcome is never held
-    ++a->forgotten;
-    a->done_cv.notify_all();
-    return CIR_OK;
-  }
-  auto r = a->done.find(ticket);
-  if (r == a->done.end())
-    return fail(CIR_ENOTFOUND, "unknown, consumed, forgotten or expired ticket");
-  a->errors.erase(ticket);
-  a->done.erase(r);
-  ++a->forgotten;
-  return CIR_OK;
+  std::string err;
+  const int rc = verify_queue(ctx)->forget(ticket, &err);
+  return rc ? fail(rc, err) : CIR_OK;
 }
 
 int cir_verify_window(cir_ctx* ctx, uint32_t window_us, uint32_t max_batch) {
   if (!ctx || max_batch == 0) return fail(CIR_EINVAL, "bad argument");
-  AsyncVerify* a = async_verify(ctx);
-  std::lock_guard<std::mutex> lk(a->mu);
-  ctx->av_window_us = window_us;
-  ctx->av_max_batch = max_batch;
+  verify_queue(ctx)->window(window_us, max_batch);
   return CIR_OK;
 }
 
 int cir_verify_limits(cir_ctx* ctx, uint64_t max_bytes, uint64_t max_results, int flags) {
   if (!ctx) return fail(CIR_EINVAL, "null ctx");
   if (flags & ~CIR_VERIFY_NONBLOCK) return fail(CIR_EINVAL, "unknown flags");
-  AsyncVerify* a = async_verify(ctx);
-  {
-    std::lock_guard<std::mutex> lk(a->mu);
-    a->max_bytes = max_bytes ? max_bytes : kVerifyMaxBytes;
-    a->max_results = max_results ? max_results : kVerifyMaxResults;
-    a->nonblocking = (flags & CIR_VERIFY_NONBLOCK) != 0;
-    a->evict();
-  }
-  a->room_cv.notify_all();
+  verify_queue(ctx)->limits(max_bytes, max_results, (flags & CIR_VERIFY_NONBLOCK) != 0);
   return CIR_OK;
 }
 
 int cir_verify_stats(cir_ctx* ctx, uint64_t out[CIR_VERIFY_STATS_FIELDS]) {
   if (!ctx || !out) return fail(CIR_EINVAL, "null pointer");
-  AsyncVerify* a = async_verify(ctx);
-  std::lock_guard<std::mutex> lk(a->mu);
-  const uint64_t v[CIR_VERIFY_STATS_FIELDS] = {a->held,      a->peak,      a->pending.size(),
-                                               a->done.size(), a->expired, a->forgotten,
-                                               a->refused,   a->batches};
-  memcpy(out, v, sizeof(v));
+  verify_queue(ctx)->stats(out);
   return CIR_OK;
 }
 

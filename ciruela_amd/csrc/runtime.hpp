@@ -15,6 +15,7 @@
 
 #include "ciruela_blockhash.h"
 #include "kernels.hpp"
+#include "verify_queue.hpp"
 
 namespace cir {
 
@@ -201,12 +202,6 @@ struct ScanStats {
 };
 }  // namespace cir
 
-namespace cir {
-struct AsyncVerify;  // runtime.cpp: cir_verify_submit's batching worker
-struct AsyncVerifyDeleter {
-  void operator()(AsyncVerify* p) const;
-};
-}  // namespace cir
 
 struct cir_ctx {
   std::vector<std::unique_ptr<cir::Device>> devs;
@@ -216,11 +211,11 @@ struct cir_ctx {
   // kernel on device 0's chain stream)
   int footer = CIR_FOOTER_HOST;
   cir::ScanStats stats;
-  // cir_verify_submit's worker, created on first use; declared last, so it
-  // is stopped (its worker joined) before anything it reads goes away
-  uint32_t av_window_us = 200, av_max_batch = 4096;
+  // cir_verify_submit's queue and worker (verify_queue.hpp), created on
+  // first use; declared last, so it is stopped (its worker drained and
+  // joined) before anything its hashing uses goes away
   std::mutex av_mu;
-  std::unique_ptr<cir::AsyncVerify, cir::AsyncVerifyDeleter> av;
+  std::unique_ptr<cir::VerifyQueue> av;
 };
 
 namespace cir {

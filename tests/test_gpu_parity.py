@@ -1900,9 +1900,10 @@ def test_verify_async_queue_is_bounded(gpu, oracle):
     """cir_verify_limits: the block bytes accepted and not yet verified never
     pass max_bytes.  Non-blocking, a submit that would pass it is CIR_EAGAIN
     and the block is not taken (deterministic here: the first block's batch
-    waits out a 100 ms window); blocking, submitters from three threads wait
-    for room.  Every accepted ticket resolves to the oracle's outcome, wrong
-    digests included, and nothing stays held."""
+    would wait out a 100 ms window; the refusal sends it to the worker at
+    once); blocking, submitters from three threads wait for room.  Every
+    accepted ticket resolves to the oracle's outcome, wrong digests
+    included, and nothing stays held."""
     import threading
     n = gpu._n
     c = gpu.Context(device_mask=1, staging_bytes=16 << 20)
@@ -1911,14 +1912,20 @@ def test_verify_async_queue_is_bounded(gpu, oracle):
     c.verify_limits(max_bytes=64 << 10, nonblocking=True)
     c.verify_window(100000)
     a, b = _blocks_with_bad(oracle, rng, 2, size=40 << 10, every=2, bad=1)  # b's digest is wrong
+    import time
     ta = c.verify_submit(a[0], a[1])
+    st = c.verify_stats()
+    assert st["bytes_held"] == 40 << 10 and st["pending"] == 1
+    t0 = time.perf_counter()
     with pytest.raises(n.CiruelaError) as e:
         c.verify_submit(b[0], b[1])
     assert e.value.status == n.CIR_EAGAIN
     t_empty = c.verify_submit(b"", oracle_digest(oracle, b""))  # 0 bytes always fit
+    assert c.verify_wait(ta) is True
+    assert time.perf_counter() - t0 < 0.08  # sealed by the refusal, not the 100 ms window
+    assert c.verify_wait(t_empty) is True
     st = c.verify_stats()
-    assert st["refused"] == 1 and st["bytes_held"] == 40 << 10 and st["pending"] == 2
-    assert c.verify_wait(ta) is True and c.verify_wait(t_empty) is True
+    assert st["refused"] == 1 and st["peak_bytes_held"] == 40 << 10
     tb = c.verify_submit(b[0], b[1])  # room again
     assert c.verify_wait(tb) is False
     # a burst through a 1 MiB bound, non-blocking with retries, then blocking
