@@ -489,6 +489,7 @@ static int run_blocks(cir_ctx* ctx, Device& d, const uint8_t* arena, const uint6
   std::lock_guard<std::mutex> lk(d.mu);
   DeviceGuard guard;
   CIR_HIP(hipSetDevice(d.id));
+  SlotDrain drain{d};  // an early return leaves no slot busy
   const uint64_t cap = ctx->staging;
   const uint64_t cap_blk = std::max<uint64_t>(cap / 512, 4096);
   const bool nt = stage_copy_nt();
@@ -599,6 +600,7 @@ static int run_file_dev(cir_ctx* ctx, Device& d, const Reader& rd, uint64_t bs,
   std::lock_guard<std::mutex> lk(d.mu);
   DeviceGuard guard;
   CIR_HIP(hipSetDevice(d.id));
+  SlotDrain drain{d};  // an early return leaves no slot busy
   uint64_t chunk = ctx->staging / bs * bs;
   if (chunk == 0) chunk = bs;
   const uint64_t chunk_blk = chunk / bs;

@@ -173,6 +173,24 @@ struct Device {
   int ensure_timing(Slot& s);
 };
 
+// Every slot a staged loop submitted is waited for before the loop lets go
+// of its device, on every return path: a loop that fails part-way (a read
+// error, a failed launch) leaves no busy slot behind -- the next loop on the
+// device would find it busy and retire it as one of its own batches (a
+// striped scan then reported a wrapped-around progress count and emitted
+// files before their digests were back).  Declare it after the device lock
+// and the DeviceGuard, so it runs first with the device current.
+struct SlotDrain {
+  Device& d;
+  ~SlotDrain() {
+    for (Slot& s : d.slot)
+      if (s.busy) {
+        (void)hipEventSynchronize(s.done);
+        s.busy = false;
+      }
+  }
+};
+
 // A batch of blocks already packed in a slot's host buffer:
 // block k = h_data[h_off[k] .. h_off[k] + h_len[k]).
 // Staging engine: the caller packs a slot, submit() uploads and hashes it

@@ -201,6 +201,7 @@ static int hash_range(cir_ctx* ctx, Device& d, size_t di, const std::vector<Scan
   std::lock_guard<std::mutex> lk(d.mu);
   DeviceGuard guard;
   CIR_HIP(hipSetDevice(d.id));
+  SlotDrain drain{d};  // an early return leaves no slot busy
   const bool stats = scan_t0 >= 0;
   struct RecordTimes {  // the device's slots are timed for this range only
     Device& d;

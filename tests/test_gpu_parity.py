@@ -1147,6 +1147,48 @@ def test_split_scan_streams_within_stripes(gpu, monkeypatch, tmp_path):
     c.close()
 
 
+def test_scan_after_a_failed_scan(gpu, oracle, monkeypatch, tmp_path):
+    """A scan that fails part-way (an unreadable file: CIR_EIO, the
+    reference's io::Error) leaves no staging slot busy (SlotDrain), so the
+    next scan on the same context is right.  Before, a slot left busy on
+    device state 1 was retired by the next scan as one of its own batches
+    with a wrapped-around progress count, which emitted files before their
+    digests were back whenever stripe 0 finished before state 1's first
+    real batch -- a race this test exercises but cannot force (the build
+    without the drain passed it on one box).  Then the host paths on the
+    same context.  Needs a non-root user (chmod 000 must deny the read)."""
+    if os.geteuid() == 0:
+        pytest.skip("root reads a chmod-000 file")
+    n = gpu._n
+    monkeypatch.setenv("CIR_DEBUG_SPLIT", "2")
+    c = gpu.Context(device_mask=1, staging_bytes=64 << 10)
+    monkeypatch.delenv("CIR_DEBUG_SPLIT")
+    monkeypatch.setenv("CIR_DEBUG_STRIPE_BLOCKS", "8")
+    rng = random.Random(65)
+    bad_root, good_root = tmp_path / "bad", tmp_path / "good"
+    for root in (bad_root, good_root):
+        (root / "d").mkdir(parents=True)
+        for k in range(96):
+            (root / "d" / ("f%03d" % k)).write_bytes(rng.randbytes(4096))
+    want = dirsig_oracle.scan(str(good_root), 4096)
+    good = gpu.ScannerConfig.new().block_size(4096).threads(2).add_dir(str(good_root), "/")
+    bad = gpu.ScannerConfig.new().block_size(4096).threads(2).add_dir(str(bad_root), "/")
+    for k in (40, 41, 43, 45, 57, 60, 75, 90):
+        f = bad_root / "d" / ("f%03d" % k)
+        f.chmod(0)
+        try:
+            with pytest.raises(n.CiruelaError) as e:
+                gpu.v1.scan(bad, context=c)
+            assert e.value.status == n.CIR_EIO, e.value
+        finally:
+            f.chmod(0o644)
+        assert gpu.v1.scan(good, context=c) == want, k
+    data = rng.randbytes(3 << 20)
+    assert c.hash_memory(data, 32768) == b"".join(
+        oracle_digest(oracle, data[i:i + 32768]) for i in range(0, len(data), 32768))
+    c.close()
+
+
 def test_error_paths_are_codes_not_aborts(gpu, small_ctx, tmp_path):
     """SURVEY.md 8b errors: bad arguments give CIR_EINVAL, unreadable sources
     CIR_EIO (the reference's io::Error), never an abort; the context stays
