@@ -1328,7 +1328,11 @@ def main():
     # which GPU each rank ran on, as its driver and its own clocks see it
     devices = distinct = devices_problem = None
     if distributed:
-        devices = gather_objects(device_identity(ca, local % ndev))
+        try:  # every rank must reach the gather, whatever its probe did
+            ident = device_identity(ca, local % ndev)
+        except Exception as e:  # noqa: BLE001 - reported in the line
+            ident = {"hip_device": local % ndev, "error": "%s: %s" % (type(e).__name__, e)}
+        devices = gather_objects(ident)
         distinct, devices_problem = devices_check(devices, args.dist_backend == "nccl")
         if devices_problem and devices_problem.startswith("FAIL"):
             parity = devices_problem if parity == "ok" else parity + "; " + devices_problem
