@@ -29,6 +29,12 @@ CPU of the affinity mask; the host record names the cgroup CPU quota.
     python bench.py --gpus 1 --force-dist   (the N>1 code path -- process
         group, config 4, job-wide parity -- on one rank, launched the same way)
 
+The N>1 line also carries devices_seen: every rank's PCI bus id, UUID and
+device clocks (cir_debug_device_identity), gathered over the process group;
+under RCCL two ranks on one device fail the line.  Config 1's CLI is timed
+before this process touches the GPU; config 5 adds a cold scan of the tree
+it has just written (value_cold) before the read passes and timed scans.
+
 config.entry_point names the C-ABI call the timed steps made:
 cir_hash_chunks_dev (the production path, --loader api, the default) or
 cir_debug_hash_uniform_dev (a single-kernel A/B variant, --loader glds|direct).
