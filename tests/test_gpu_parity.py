@@ -547,6 +547,24 @@ def test_cli_sync(gpu, tmp_path, teardown):
     assert b"Indexed" in p.stderr
 
 
+def test_cli_exits_normally_under_a_profiler(gpu, tmp_path):
+    """With a profiler's environment (ROCPROF_* / ROCP_TOOL_LIBRARIES, as
+    rocprofv3 sets for its tool library) `ciruela-index` skips cir_destroy
+    but returns from main, so exit handlers -- where the tool writes its
+    trace -- still run; the output is the same."""
+    import subprocess
+    from conftest import ROOT
+    make_tree(tmp_path / "src")
+    env = dict(os.environ, CIR_TRACE="1", ROCPROF_CIRUELA_TEST="1")
+    p = subprocess.run([os.path.join(ROOT, "bin", "ciruela-index"), "sync",
+                        "--append", str(tmp_path / "src") + ":/dest"], env=env,
+                       capture_output=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert b"profiler present: normal exit" in p.stderr
+    want = dirsig_oracle.scan(str(tmp_path / "src"), 32768)
+    assert want.endswith(p.stdout.split()[0] + b"\n")
+
+
 def test_cli_hash(gpu, oracle, tmp_path):
     """`ciruela-index hash FILE...` (the per-file Hashes::hash_file list):
     every line -- path, size, one digest per block -- equal to the oracle,
