@@ -22,7 +22,7 @@ OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS_HIP)) \
         $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(SRCS_CPP))
 HDRS := $(wildcard $(CSRC)/*.hpp) include/ciruela_blockhash.h
 
-all: $(LIB) $(CLI) build/hash_bytes_conc oracle
+all: $(LIB) $(CLI) build/hash_bytes_conc build/verify_daemon_sim oracle
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -43,6 +43,12 @@ $(CLI): $(CSRC)/cli.cpp $(LIB) $(HDRS)
 
 # concurrent hash_bytes callers from C threads (tools/hash_bytes_conc.cpp)
 build/hash_bytes_conc: tools/hash_bytes_conc.cpp $(LIB) include/ciruela_blockhash.h
+	@mkdir -p build
+	$(HIPCC) $(HOSTFLAGS) $< -o $@ -Lciruela_amd -lciruela_amd \
+	    -Wl,-rpath,'$$ORIGIN/../ciruela_amd' -lpthread
+
+# the daemon's per-block verify under load (tools/verify_daemon_sim.cpp)
+build/verify_daemon_sim: tools/verify_daemon_sim.cpp $(LIB) include/ciruela_blockhash.h
 	@mkdir -p build
 	$(HIPCC) $(HOSTFLAGS) $< -o $@ -Lciruela_amd -lciruela_amd \
 	    -Wl,-rpath,'$$ORIGIN/../ciruela_amd' -lpthread

@@ -95,7 +95,7 @@ class VerifyQueue {
         b = it->get();
         break;
       }
-    if (b && b->arena.size() + n > b->arena.capacity()) {
+    if (b && b->used + n > b->cap) {
       b->sealed = true;  // full: this block opens the next batch
       b = nullptr;
     }
@@ -103,15 +103,17 @@ class VerifyQueue {
       auto nb = std::make_unique<Batch>();
       nb->ht = ht;
       // one batch's arena: half the byte bound, so a batch can form while
-      // the previous one is verified (reserved once: appends never move it)
-      nb->arena.reserve(std::max<uint64_t>(n, std::max<uint64_t>(1, max_bytes_ / 2)));
+      // the previous one is verified; a spare arena of a verified batch is
+      // reused (its pages are already faulted in)
+      arena_for(*nb, std::max<uint64_t>(n, std::max<uint64_t>(1, max_bytes_ / 2)));
       nb->first = std::chrono::steady_clock::now();
       b = nb.get();
       queue_.push_back(std::move(nb));
     }
-    b->off.push_back(b->arena.size());
+    const uint64_t at = b->used;
+    b->used += n;
+    b->off.push_back(at);
     b->len.push_back((uint32_t)n);
-    b->arena.insert(b->arena.end(), data, data + n);
     b->expected.insert(b->expected.end(), expected, expected + 32);
     const uint64_t t = next_ticket_++;
     b->tickets.push_back(t);
@@ -120,8 +122,14 @@ class VerifyQueue {
     held_ += n;
     peak_ = std::max(peak_, held_);
     *ticket = t;
+    // the block's bytes are copied outside the lock, into the space just
+    // reserved; the worker hashes a batch only once its writers are done
+    ++b->writers;
     lk.unlock();
     cv_.notify_one();
+    if (n) memcpy(b->arena.get() + at, data, n);
+    lk.lock();
+    if (--b->writers == 0) writers_cv_.notify_all();
     return CIR_OK;
   }
 
@@ -206,7 +214,9 @@ class VerifyQueue {
   // one arena as they were submitted
   struct Batch {
     int ht = 0;
-    std::vector<uint8_t> arena;
+    std::unique_ptr<uint8_t[]> arena;  // cap bytes, the first `used` taken
+    uint64_t cap = 0, used = 0;
+    int writers = 0;  // submitters still copying into the arena
     std::vector<uint64_t> off;
     std::vector<uint32_t> len;
     std::vector<uint8_t> expected;
@@ -227,6 +237,20 @@ class VerifyQueue {
     return r;
   }
 
+  // b gets an arena of at least `bytes`: a spare one when one is big enough
+  // (caller holds mu_)
+  void arena_for(Batch& b, uint64_t bytes) {
+    for (auto it = spare_.begin(); it != spare_.end(); ++it)
+      if (it->second >= bytes) {
+        b.arena = std::move(it->first);
+        b.cap = it->second;
+        spare_.erase(it);
+        return;
+      }
+    b.arena.reset(new uint8_t[bytes]);  // not value-initialised: untouched pages cost nothing
+    b.cap = bytes;
+  }
+
   void evict() {  // caller holds mu_
     while (done_.size() > max_results_) {
       errors_.erase(done_.begin()->first);
@@ -238,6 +262,10 @@ class VerifyQueue {
   void run() {
     std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
+      // idle for a second with spare arenas: give their memory back
+      if (queue_.empty() && !stop_ && !spare_.empty() &&
+          !cv_.wait_for(lk, std::chrono::seconds(1), [&] { return stop_ || !queue_.empty(); }))
+        spare_.clear();
       cv_.wait(lk, [&] { return stop_ || !queue_.empty(); });
       if (queue_.empty()) return;  // stopped and drained
       Batch* b = queue_.front().get();
@@ -246,14 +274,15 @@ class VerifyQueue {
       std::unique_ptr<Batch> bp = std::move(queue_.front());
       queue_.pop_front();
       bp->sealed = true;  // (no more appends)
+      writers_cv_.wait(lk, [&] { return bp->writers == 0; });  // every block copied in
       lk.unlock();
       const size_t n = bp->tickets.size();
       std::vector<uint8_t> got(32 * n);
       static const uint8_t empty = 0;
       std::string err;
-      const int rc = hash_(bp->ht, bp->arena.empty() ? &empty : bp->arena.data(), bp->off.data(),
+      const int rc = hash_(bp->ht, bp->used ? bp->arena.get() : &empty, bp->off.data(),
                            bp->len.data(), n, got.data(), &err);
-      const uint64_t bytes = bp->arena.size();
+      const uint64_t bytes = bp->used;
       lk.lock();
       for (size_t i = 0; i < n; ++i) {
         const uint64_t t = bp->tickets[i];
@@ -268,21 +297,26 @@ class VerifyQueue {
       held_ -= bytes;
       ++batches_;
       evict();
+      // keep the arena for a later batch (at most two spares, within the
+      // byte bound's two batches); the rest is freed outside the lock
+      if (spare_.size() < 2 && bp->cap <= std::max<uint64_t>(1, max_bytes_ / 2))
+        spare_.emplace_back(std::move(bp->arena), bp->cap);
       room_cv_.notify_all();
       done_cv_.notify_all();
       lk.unlock();
-      bp.reset();  // the arena is freed outside the lock
+      bp.reset();
       lk.lock();
     }
   }
 
   HashFn hash_;
   std::mutex mu_;
-  std::condition_variable cv_, done_cv_, room_cv_;
+  std::condition_variable cv_, done_cv_, room_cv_, writers_cv_;
   std::deque<std::unique_ptr<Batch>> queue_;
   std::unordered_set<uint64_t> pending_;  // submitted, outcome not yet known
   std::map<uint64_t, int> done_;          // outcome held: 1 match, 2 mismatch, < 0 error
   std::unordered_map<uint64_t, std::string> errors_;
+  std::vector<std::pair<std::unique_ptr<uint8_t[]>, uint64_t>> spare_;  // arenas and sizes
   uint64_t next_ticket_ = 1;
   uint64_t held_ = 0, peak_ = 0;  // block bytes accepted and not yet verified
   uint64_t max_bytes_ = kMaxBytes, max_results_ = kMaxResults;

@@ -252,6 +252,13 @@ static void deterministic(std::mt19937_64& rng) {
   th.release();
   CHECK(q.wait(u1, &err) == 1 && q.wait(u2, &err) == 1);
   CHECK(th.batches.load() - b0 == 2);
+  // idle past a second: the spare arenas are given back, and the queue
+  // works as before afterwards
+  stage("idle trim");
+  std::this_thread::sleep_for(std::chrono::milliseconds(1200));
+  uint64_t tz = 0;
+  CHECK(q.submit(1, big.data.data(), big.data.size(), big.expected, &tz, &err) == 0);
+  CHECK(q.wait(tz, &err) == 1);
 }
 
 // random traffic from several threads against a byte bound, blocking or
