@@ -821,6 +821,16 @@ def run_config5(args, ca, ctx, ctx_init_s=None):
             index = bytes(got)
         del got
     ctx.set_footer_mode(ctx.FOOTER_HOST)
+    # row f1 at full size: RawIndex::into_mut + to_raw_data of this index
+    # (cir_index_rewrite: parse, rebuild the tree, re-emit, re-hash the
+    # footer) must give the same bytes (the reference's roundtrip property,
+    # src/cluster/download.rs:368-382)
+    t0 = time.perf_counter()
+    rewritten = ctx.index_rewrite(index)
+    rw_s = time.perf_counter() - t0
+    rewrite = {"seconds": round(rw_s, 4), "index_mb_per_s": round(len(index) / rw_s / 1e6, 1),
+               "identical": rewritten == index}
+    del rewritten
     times = [sc["seconds"] for sc in scans if sc["footer"] == modes[0]]
     best = min(times)
     best_scan = min((sc for sc in scans if sc["footer"] == modes[0]), key=lambda sc: sc["seconds"])
@@ -901,7 +911,9 @@ def run_config5(args, ca, ctx, ctx_init_s=None):
                       for sc in scans],
             "files": nfiles, "bytes": nbytes, "index_bytes": len(index),
             "image_id": ca.get_hash(index).hex(),
-            "matches_oracle": index == want and cold.get("matches_oracle", True),
+            "matches_oracle": (index == want and cold.get("matches_oracle", True)
+                               and rewrite["identical"]),
+            "index_rewrite": rewrite,
             "tree_gen_s": round(gen_s, 1),
             "reader_threads": threads or "auto (min(12, 3/4 of the CPU share))",
             "tree": args.tree_dir,
