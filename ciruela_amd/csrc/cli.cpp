@@ -168,12 +168,23 @@ int main(int argc, char** argv) {
   const uint64_t staging = staging_for(total);
   const char* tv = getenv("CIR_TRACE");
   const bool trace = tv && *tv && strcmp(tv, "0") != 0;
+  // An input below one staging slot is one small batch: its copies go
+  // through the runtime's blit kernels instead of the SDMA engines, whose
+  // first use in a process costs ~16-17 ms (cir_init's first uploads) -- a
+  // tenth of a one-shot `sync` of config 1's 10 MiB tree
+  // (profiles/r05/cli_sdma_ab.log).  Large inputs keep SDMA (the link's full
+  // rate); a caller's own HSA_ENABLE_SDMA wins.  Set before the first HIP
+  // call, when the runtime reads it.
+  const bool small = staging != 0;
+  if (small && !getenv("HSA_ENABLE_SDMA")) setenv("HSA_ENABLE_SDMA", "0", 0);
   auto ms_since = [](std::chrono::steady_clock::time_point t) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
   };
   if (trace) {
-    fprintf(stderr, "ciruela-index: staging %llu bytes per slot (0 = library default)\n",
-            (unsigned long long)staging);
+    fprintf(stderr, "ciruela-index: staging %llu bytes per slot (0 = library default), %s copies\n",
+            (unsigned long long)staging,
+            strcmp(getenv("HSA_ENABLE_SDMA") ? getenv("HSA_ENABLE_SDMA") : "1", "0") == 0
+                ? "blit" : "SDMA");
     // the HIP runtime's own start-up (device discovery), apart from cir_init
     const auto t0 = std::chrono::steady_clock::now();
     const int n = cir_device_count();

@@ -561,6 +561,7 @@ def test_cli_exits_normally_under_a_profiler(gpu, tmp_path):
                        capture_output=True, timeout=120)
     assert p.returncode == 0, p.stderr
     assert b"profiler present: normal exit" in p.stderr
+    assert b"blit copies" in p.stderr  # a small input skips the SDMA engines' start-up
     want = dirsig_oracle.scan(str(tmp_path / "src"), 32768)
     assert want.endswith(p.stdout.split()[0] + b"\n")
 
@@ -609,6 +610,7 @@ def test_cli_opens_devices_for_its_input(gpu, tmp_path, mib, states):
                         "--append", str(src) + ":/dest", "--index-dir", str(tmp_path)],
                        env=env, capture_output=True, timeout=120)
     assert p.returncode == 0, p.stderr[-3000:]
+    assert "SDMA copies" in p.stderr.decode()  # a large input keeps the link's full rate
     line = [ln for ln in p.stderr.decode().splitlines() if "device(s) for" in ln]
     assert line and (" %d device(s) for %d input bytes" % (states, 4 * per + 6000)) in line[0], \
         line
