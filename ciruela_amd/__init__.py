@@ -18,6 +18,11 @@ get_hash                        dir_signature::get_hash (src/index.rs:99)
 InMemoryIndexes                 ciruela::index::InMemoryIndexes (src/index.rs:53)
 ThreadedBlockReader             ciruela::blocks::ThreadedBlockReader
                                 (src/blocks.rs:85)
+Context.verify_blocks[_dev]     FetchBlock::poll's `hash_bytes(..) == blk.hash`
+                                (src/daemon/tracking/fetch_blocks.rs:77), batched
+Context.verify_submit / poll /  the same check per block, batched by the library,
+  wait / forget / limits        bounded (CIR_EAGAIN backpressure, forgotten tickets)
+Context.check_file              Hashes::check_file (src/daemon/disk/commit.rs:104)
 =============================  ==============================================
 
 All hashing runs on gfx950 through the library; there is no CPU fallback.
