@@ -215,7 +215,8 @@ static int hash_range(cir_ctx* ctx, Device& d, size_t di, const std::vector<Scan
     ref_ms = now_ms() - scan_t0;
   }
   std::vector<std::array<double, kScanBatchFields>> rows;
-  const uint64_t cap = std::max<uint64_t>(ctx->staging, bs + 16);
+  // (a multiple of 16: file segments start 16-byte aligned)
+  const uint64_t cap = (std::max<uint64_t>(ctx->staging, bs + 16) + 15) & ~15ull;
   const uint64_t cap_blk = std::max<uint64_t>(cap / 512, 4096);
   // the first batches ramp up (1/8, 1/4, 1/2 of a slot, then whole slots):
   // the first upload starts after a short read instead of a whole slot's,
@@ -298,6 +299,7 @@ static int hash_range(cir_ctx* ctx, Device& d, size_t di, const std::vector<Scan
       if (rc) return rc;
       std::vector<ReadJob> jobs;
       uint64_t pos = 0, n = 0;
+      uint64_t used = 0;  // end of the last segment packed (pos may be aligned past it)
       const uint64_t first = files[fi].first_blk + fblk;
       while (more_here() && n < cap_blk) {
         const ScanFile& f = files[fi];
@@ -319,6 +321,7 @@ static int hash_range(cir_ctx* ctx, Device& d, size_t di, const std::vector<Scan
           jobs.push_back({fi, off0 + piece, std::min<uint64_t>(kReadPiece, bytes - piece),
                           s.h_data + pos + piece});
         pos += bytes;
+        used = pos;
         n += take;
         fblk += take;
       }
@@ -327,17 +330,21 @@ static int hash_range(cir_ctx* ctx, Device& d, size_t di, const std::vector<Scan
       rc = run_reads(jobs, files, threads);
       if (rc) return rc;
       const double t_read1 = clock ? now_ms() : 0;
-      rc = slot_submit(d, s, std::max<uint64_t>(pos, 16), n, ht);
+      // the packed bytes only: a break after aligning `pos` for the next
+      // segment must not send the slot's end (round 4 sent up to 15 bytes
+      // past a slot whose size was not a multiple of 16: a block size above
+      // the staging size failed the upload)
+      rc = slot_submit(d, s, std::max<uint64_t>(used, 16), n, ht);
       if (rc) return rc;
       if (trace_on())
         fprintf(stderr, "cir_scan dev %d batch: %.1f MiB, %zu jobs, wait %.2f ms, read %.2f ms (%.1f GB/s)\n",
-                d.id, pos / 1048576.0, jobs.size(), t_wait1 - t_wait0, t_read1 - t_read0,
-                pos / 1e6 / std::max(t_read1 - t_read0, 1e-3));
+                d.id, used / 1048576.0, jobs.size(), t_wait1 - t_wait0, t_read1 - t_read0,
+                used / 1e6 / std::max(t_read1 - t_read0, 1e-3));
       pending_first[k] = first;
       pending_n[k] = n;
       pending_range[k] = ri;
       if (stats) {
-        pending_row[k][0] = (double)pos;
+        pending_row[k][0] = (double)used;
         pending_row[k][1] = (double)n;
         pending_row[k][2] = t_wait1 - t_wait0;
         pending_row[k][3] = t_read0 - scan_t0;

@@ -1788,6 +1788,49 @@ def test_context_lifecycle_releases_device_memory(gpu, oracle):
     assert rss() - rss0 < (64 << 20), (rss() - rss0) >> 20
 
 
+def test_blocks_larger_than_the_staging_slot(gpu, oracle, tmp_path):
+    """A block size (and single blocks) larger than the context's staging
+    slot: the slots grow to one block (scan, hash_file, hash_memory,
+    hash_blocks, the asynchronous verify); every digest and the index equal
+    the oracles'.  bs = 3 MiB + 5 on 1 MiB slots.  Until round 5 the scan
+    sent a batch's 16-byte-aligned end instead of its packed bytes, past the
+    end of a slot sized bs + 16 (not a multiple of 16): the upload failed
+    with an invalid argument."""
+    c = gpu.Context(device_mask=1, staging_bytes=1 << 20)
+    rng = random.Random(91)
+    bs = (3 << 20) + 5
+    root = tmp_path / "tree"
+    (root / "d").mkdir(parents=True)
+    sizes = [0, 1, bs, bs + 1, 2 * bs + 100, (10 << 20) + 7]
+    for k, n in enumerate(sizes):
+        (root / "d" / ("f%d" % k)).write_bytes(rng.randbytes(n))
+    cfg = gpu.ScannerConfig.new().block_size(bs).threads(3).add_dir(str(root), "/")
+    assert gpu.v1.scan(cfg, context=c) == dirsig_oracle.scan(str(root), bs)
+    data = (root / "d" / "f5").read_bytes()
+    want = b"".join(oracle_digest(oracle, data[i:i + bs]) for i in range(0, len(data), bs))
+    assert c.hash_memory(data, bs) == want
+    with open(root / "d" / "f5", "rb") as f:
+        size, hashes = c.hash_file(f.fileno(), bs)
+    assert size == len(data) and hashes == want
+    lens = [5 << 20, 1, 0, (2 << 20) + 3]
+    offs = [0, 17, 40, 123]
+    got = c.hash_blocks(data, offs, lens)
+    assert got == b"".join(oracle_digest(oracle, data[o:o + n]) for o, n in zip(offs, lens))
+    t = c.verify_submit(data[:5 << 20], oracle_digest(oracle, data[:5 << 20]))
+    assert c.verify_wait(t) is True
+    c.close()
+    # a staging size that is not a multiple of 16 (the scan's segments are
+    # 16-byte aligned inside a slot): random trees at two block sizes
+    c = gpu.Context(device_mask=1, staging_bytes=1000003)
+    for k, bs2 in enumerate((4096, 65536 + 3)):
+        root2 = tmp_path / ("odd%d" % k)
+        root2.mkdir()
+        random_tree(root2, rng, bs2)
+        cfg = gpu.ScannerConfig.new().block_size(bs2).threads(2).add_dir(str(root2), "/")
+        assert gpu.v1.scan(cfg, context=c) == dirsig_oracle.scan(str(root2), bs2), bs2
+    c.close()
+
+
 def random_tree(root, rng, bs):
     """A random tree for the scan sweep: nested directories, files whose
     sizes sit on and around block and 128-B line edges (empty files
@@ -1816,12 +1859,15 @@ def random_tree(root, rng, bs):
 
 def scan_case(gpu, seed, tmp_path, monkeypatch):
     """One randomized end-to-end scan against the scan oracle, over the
-    scan's knobs: block size, hash type, reader threads, staging size, the
+    scan's knobs: block size (up to one above the staging size), hash type,
+    reader threads, staging size (one not a multiple of 16), the
     staging copy mode, the footer's placement, a split over 1-3 device
     states (CIR_DEBUG_SPLIT on the one GPU) with stripes of 1-5 blocks or the
     default, and the index returned whole or written out as it goes."""
     rng = random.Random(seed)
-    bs = rng.choice([128, 1000, 4096, 32768, 65536 + 3])
+    # (1 MiB + 5: a block above the smallest staging size, in a slot whose
+    # size is not a multiple of 16)
+    bs = rng.choice([128, 1000, 4096, 32768, 65536 + 3, (1 << 20) + 5])
     root = tmp_path / ("t%d" % seed)
     root.mkdir()
     random_tree(root, rng, bs)
@@ -1834,7 +1880,8 @@ def scan_case(gpu, seed, tmp_path, monkeypatch):
         # them a few blocks long so small trees cross many stripe edges
         monkeypatch.setenv("CIR_DEBUG_STRIPE_BLOCKS", str(rng.choice([0, 1, 2, 5])))
     try:
-        ctx = gpu.Context(device_mask=1, staging_bytes=rng.choice([1 << 20, 3 << 20, 16 << 20]))
+        ctx = gpu.Context(device_mask=1,
+                          staging_bytes=rng.choice([1 << 20, 1000003, 3 << 20, 16 << 20]))
     finally:
         monkeypatch.delenv("CIR_DEBUG_SPLIT", raising=False)
     ctx.set_footer_mode(rng.choice([ctx.FOOTER_HOST, ctx.FOOTER_GPU]))
