@@ -595,18 +595,27 @@ struct HashBuf {
   }
 };
 
+// size_hint: the source's length when known (a lower bound for a file that
+// may grow); `exact`: the source ends there (memory, a known range).
 static int run_file_dev(cir_ctx* ctx, Device& d, const Reader& rd, uint64_t bs,
-                        uint64_t* size_out, HashBuf& hashes, int ht, uint64_t size_hint = 0) {
+                        uint64_t* size_out, HashBuf& hashes, int ht, uint64_t size_hint = 0,
+                        bool exact = false) {
   std::lock_guard<std::mutex> lk(d.mu);
   DeviceGuard guard;
   CIR_HIP(hipSetDevice(d.id));
   SlotDrain drain{d};  // an early return leaves no slot busy
   uint64_t chunk = ctx->staging / bs * bs;
   if (chunk == 0) chunk = bs;
-  const uint64_t chunk_blk = chunk / bs;
+  // an exact source shorter than one block is one short block: a slot of
+  // its own size, not of the block size (a huge block size over a small
+  // input would otherwise pin and allocate a block-sized slot)
+  const bool one_short = exact && size_hint < bs;
+  if (one_short) chunk = std::max<uint64_t>(16, (size_hint + 15) & ~15ull);
+  const uint64_t chunk_blk = one_short ? 1 : chunk / bs;
   // the first batches ramp up (1/8, 1/4, 1/2 of a slot, then whole slots),
   // as the scan's do: the first upload starts after a short fill
-  uint64_t fill = scan_ramp() ? std::max<uint64_t>(bs, chunk / 8 / bs * bs) : chunk;
+  uint64_t fill = one_short ? chunk
+                            : scan_ramp() ? std::max<uint64_t>(bs, chunk / 8 / bs * bs) : chunk;
   uint64_t total = 0;
   bool eof = false;
   size_t pending_at[2] = {0, 0}, pending_n[2] = {0, 0};
@@ -661,8 +670,8 @@ static int run_file_dev(cir_ctx* ctx, Device& d, const Reader& rd, uint64_t bs,
 }
 
 static int run_file(cir_ctx* ctx, const Reader& rd, uint64_t bs, uint64_t* size_out,
-                    HashBuf& hashes, int ht, uint64_t size_hint = 0) {
-  return run_file_dev(ctx, *ctx->devs[0], rd, bs, size_out, hashes, ht, size_hint);
+                    HashBuf& hashes, int ht, uint64_t size_hint = 0, bool exact = false) {
+  return run_file_dev(ctx, *ctx->devs[0], rd, bs, size_out, hashes, ht, size_hint, exact);
 }
 
 // read(dst, n, off): exactly n bytes at offset off (known to exist), or < 0.
@@ -699,7 +708,7 @@ static int run_split(cir_ctx* ctx, const PosReader& prd, uint64_t total, uint64_
       };
       HashBuf h;
       uint64_t got = 0;
-      rc[i] = run_file_dev(ctx, *ctx->devs[i], rd, bs, &got, h, ht, end - beg);
+      rc[i] = run_file_dev(ctx, *ctx->devs[i], rd, bs, &got, h, ht, end - beg, /*exact=*/true);
       if (!rc[i] && h.len != 32 * (hi[i] - lo[i])) rc[i] = fail(CIR_EIO, "short range");
       if (rc[i])
         err[i] = t_last_error;
@@ -1351,7 +1360,7 @@ int cir_hash_memory_ht(cir_ctx* ctx, int hash_type, const uint8_t* data, uint64_
     return (int64_t)k;
   };
   HashBuf h;
-  int rc = run_file(ctx, rd, block_size, &got_size, h, hash_type, size);
+  int rc = run_file(ctx, rd, block_size, &got_size, h, hash_type, size, /*exact=*/true);
   if (rc) return rc;
   return export_hashes(h, hashes_out, nhash_out);
 }

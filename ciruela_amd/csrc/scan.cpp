@@ -215,13 +215,18 @@ static int hash_range(cir_ctx* ctx, Device& d, size_t di, const std::vector<Scan
     ref_ms = now_ms() - scan_t0;
   }
   std::vector<std::array<double, kScanBatchFields>> rows;
-  // (a multiple of 16: file segments start 16-byte aligned)
-  const uint64_t cap = (std::max<uint64_t>(ctx->staging, bs + 16) + 15) & ~15ull;
+  // A slot holds at least one block; a block is never longer than the
+  // largest file, so a huge block size over small files does not grow the
+  // slots to the block size.  (A multiple of 16: segments start 16-byte
+  // aligned.)
+  uint64_t seg = 0;
+  for (const ScanFile& f : files) seg = std::max(seg, std::min<uint64_t>(f.size, bs));
+  const uint64_t cap = (std::max<uint64_t>(ctx->staging, seg + 16) + 15) & ~15ull;
   const uint64_t cap_blk = std::max<uint64_t>(cap / 512, 4096);
   // the first batches ramp up (1/8, 1/4, 1/2 of a slot, then whole slots):
   // the first upload starts after a short read instead of a whole slot's,
   // and each read still finishes within the previous upload
-  uint64_t fill = scan_ramp() ? std::max<uint64_t>(bs + 16, cap >> 3) : cap;
+  uint64_t fill = scan_ramp() ? std::max<uint64_t>(seg + 16, cap >> 3) : cap;
   size_t ri = 0;  // the range being packed
   uint64_t b0 = 0, b1 = 0;
   size_t fi = 0;

@@ -1831,6 +1831,43 @@ def test_blocks_larger_than_the_staging_slot(gpu, oracle, tmp_path):
     c.close()
 
 
+def test_extreme_block_sizes(gpu, oracle, tmp_path):
+    """Block sizes at both ends of 1 .. 2^32-1: 1 and 7 bytes (a digest per
+    byte or seven), and 2^32-1 over small inputs -- one short block per file,
+    in slots sized to the input, not the block size (the process's resident
+    memory grows by far less than one such block).  Scan, hash_memory,
+    hash_file; every digest and the index equal the oracles'."""
+    c = gpu.Context(device_mask=1, staging_bytes=1 << 20)
+    rng = random.Random(93)
+
+    def rss():
+        with open("/proc/self/status") as f:
+            return next(int(ln.split()[1]) << 10 for ln in f if ln.startswith("VmRSS:"))
+    for bs in (1, 7, (1 << 32) - 1):
+        root = tmp_path / ("bs%d" % bs)
+        (root / "d").mkdir(parents=True)
+        for k, n in enumerate((0, 1, 7, 8, 1000, 5000)):
+            (root / "d" / ("f%d" % k)).write_bytes(rng.randbytes(n))
+        rss0 = rss()
+        cfg = gpu.ScannerConfig.new().block_size(bs).threads(2).add_dir(str(root), "/")
+        assert gpu.v1.scan(cfg, context=c) == dirsig_oracle.scan(str(root), bs), bs
+        data = rng.randbytes(3000)
+        want = b"".join(oracle_digest(oracle, data[i:i + bs]) for i in range(0, len(data), bs))
+        assert c.hash_memory(data, bs) == want, bs
+        assert rss() - rss0 < (512 << 20), (bs, (rss() - rss0) >> 20)
+        if bs > (1 << 30):
+            # a regular file may grow while hash_file reads it to EOF, so that
+            # path keeps one block-sized slot (4 GiB pinned here): not run
+            continue
+        p = root / "d" / "f5"
+        with open(p, "rb") as f:
+            size, hashes = c.hash_file(f.fileno(), bs)
+        blob = p.read_bytes()
+        assert size == 5000 and hashes == b"".join(
+            oracle_digest(oracle, blob[i:i + bs]) for i in range(0, len(blob), bs)), bs
+    c.close()
+
+
 def random_tree(root, rng, bs):
     """A random tree for the scan sweep: nested directories, files whose
     sizes sit on and around block and 128-B line edges (empty files
