@@ -63,11 +63,14 @@ def _buf(data):
 class Context:
     """A cir_ctx: the devices the host-memory entry points run on."""
 
-    def __init__(self, device_mask=0, staging_bytes=0, max_devices=0):
+    def __init__(self, device_mask=0, staging_bytes=0, max_devices=0, one_shot=False):
         """max_devices: open at most that many of the masked devices (0 = all;
-        cir_init_n).  devices_for_bytes() gives the count an input can use."""
+        cir_init_n).  devices_for_bytes() gives the count an input can use.
+        one_shot: CIR_INIT_ONE_SHOT -- one stream and one staging slot per
+        device, for one short job (the CLI's small inputs)."""
         h = ctypes.c_void_p()
-        _n.check(_n.lib.cir_init_n(ctypes.byref(h), device_mask, staging_bytes, max_devices))
+        _n.check(_n.lib.cir_init_n(ctypes.byref(h), device_mask, staging_bytes, max_devices,
+                                   _n.CIR_INIT_ONE_SHOT if one_shot else 0))
         self._h = h
 
     @staticmethod

@@ -46,6 +46,7 @@ CIR_EUNSUPPORTED = -9
 CIR_EAGAIN = -10
 CIR_VERIFY_NONBLOCK = 1
 CIR_VERIFY_STATS_FIELDS = 8
+CIR_INIT_ONE_SHOT = 1  # cir_init_n: one stream and one staging slot per device
 CIR_STAGING_LAZY = (1 << 64) - 1  # cir_init: no staging slots until a host path needs them
 
 CIR_HASH_BLAKE2B_256 = 1
@@ -58,7 +59,7 @@ WRITE_FN = ctypes.CFUNCTYPE(ctypes.c_int, c_vp, c_vp, ctypes.c_size_t)
 _SIGS = {
     "cir_init": (ctypes.c_int, [ctypes.POINTER(c_vp), ctypes.c_uint32, ctypes.c_uint64]),
     "cir_init_n": (ctypes.c_int, [ctypes.POINTER(c_vp), ctypes.c_uint32, ctypes.c_uint64,
-                                  ctypes.c_uint32]),
+                                  ctypes.c_uint32, ctypes.c_uint32]),
     "cir_devices_for_bytes": (ctypes.c_uint32, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]),
     "cir_destroy": (None, [c_vp]),
     "cir_device_count": (ctypes.c_int, []),

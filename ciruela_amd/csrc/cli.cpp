@@ -197,7 +197,10 @@ int main(int argc, char** argv) {
   // staging at start-up, include/ciruela_blockhash.h)
   const uint32_t ndev = cir_devices_for_bytes(total, staging, 32);
   const auto t_init = std::chrono::steady_clock::now();
-  int rc = cir_init_n(&ctx, 0, staging, ndev);
+  // and a small input is one short job: one stream and one slot per device
+  // (CIR_INIT_ONE_SHOT; the other streams' hardware queues were ~25 ms of
+  // cir_init, profiles/r05/start_env.log)
+  int rc = cir_init_n(&ctx, 0, staging, ndev, small ? CIR_INIT_ONE_SHOT : 0u);
   if (rc) return die(rc, "cir_init");
   if (trace) {
     int ids[64];

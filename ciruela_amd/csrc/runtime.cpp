@@ -83,7 +83,7 @@ Device::~Device() {
   (void)hipFree(single_desc_d);
   if (single) (void)hipStreamDestroy(single);
   if (compute) (void)hipStreamDestroy(compute);
-  if (copy) (void)hipStreamDestroy(copy);
+  if (copy && copy != compute) (void)hipStreamDestroy(copy);
 }
 
 bool trace_enabled() {
@@ -305,9 +305,9 @@ static int ensure_relay(Device& d) {
 
 // The part streams and their events, created by cir_init (caller holds
 // d.order_mu with d's device current).
-static int ensure_part_streams(Device& d) {
+static int ensure_part_streams(Device& d, bool quad_stream) {
   if (d.order_free) return CIR_OK;
-  CIR_HIP(create_part_streams(d));
+  if (quad_stream) CIR_HIP(create_part_streams(d));
   CIR_HIP(hipEventCreateWithFlags(&d.part_fork, hipEventDisableTiming));
   CIR_HIP(hipEventCreateWithFlags(&d.q_join, hipEventDisableTiming));
   CIR_HIP(hipEventCreateWithFlags(&d.order_free, hipEventDisableTiming));
@@ -748,7 +748,7 @@ static int export_hashes(HashBuf& h, uint8_t** out, size_t* n) {
 //     compute stream, which load the code object and touch every buffer;
 //   * one small upload on the staging and on the footer-chain stream.
 // Caller holds a DeviceGuard.
-static int init_device(Device& d, uint64_t staging, bool lazy) {
+static int init_device(Device& d, uint64_t staging, bool lazy, bool one_shot) {
   // CIR_TRACE: each step's ms on stderr (the one-shot CLI's start-up budget)
   const bool tr = trace_enabled();
   auto t = std::chrono::steady_clock::now();
@@ -761,21 +761,27 @@ static int init_device(Device& d, uint64_t staging, bool lazy) {
   };
   CIR_HIP(hipSetDevice(d.id));
   CIR_HIP(hipStreamCreateWithFlags(&d.compute, hipStreamNonBlocking));
-  CIR_HIP(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
-  CIR_HIP(hipStreamCreateWithFlags(&d.chain, hipStreamNonBlocking));
+  // one-shot: uploads share the compute stream, the footer-chain stream is
+  // created by the first GPU-footer scan (scan.cpp), no quad-part stream
+  if (one_shot)
+    d.copy = d.compute;
+  else {
+    CIR_HIP(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
+    CIR_HIP(hipStreamCreateWithFlags(&d.chain, hipStreamNonBlocking));
+  }
   CIR_HIP(hipMalloc(&d.chain_state, 16 * 8));
   for (int b = 0; b < 2; ++b)
     CIR_HIP(hipEventCreateWithFlags(&d.chain_done[b], hipEventDisableTiming));
   {
     std::lock_guard<std::mutex> lk(d.order_mu);
-    int rc = ensure_part_streams(d);
+    int rc = ensure_part_streams(d, !one_shot);
     if (rc == CIR_OK) rc = ensure_relay(d);
     if (rc) return rc;
   }
   step("streams, events, relay scratch");
   const uint64_t cap_blk = std::max<uint64_t>(staging / 512, 4096);
   const uint64_t slot_bytes = lazy ? (64ull << 10) : std::max<uint64_t>(staging, 16);
-  for (int k = 0; k < (lazy ? 2 : Device::kSlots); ++k) {
+  for (int k = 0; k < (one_shot ? 1 : lazy ? 2 : Device::kSlots); ++k) {
     const int rc = d.ensure_slot(d.slot[k], slot_bytes, lazy ? 4096 : cap_blk);
     if (rc) return rc;
   }
@@ -798,27 +804,29 @@ static int init_device(Device& d, uint64_t staging, bool lazy) {
   // footer-chain streams, with copies big enough to take the DMA engine path
   const size_t warm = (size_t)std::min<uint64_t>(slot_bytes, 4ull << 20);
   CIR_HIP(hipMemcpyAsync(s.d_data, s.h_data, warm, hipMemcpyHostToDevice, d.copy));
-  CIR_HIP(hipMemcpyAsync(d.slot[1].d_data, d.slot[1].h_data, warm, hipMemcpyHostToDevice,
-                         d.chain));
+  if (d.chain)
+    CIR_HIP(hipMemcpyAsync(d.slot[1].d_data, d.slot[1].h_data, warm, hipMemcpyHostToDevice,
+                           d.chain));
   CIR_HIP(hipStreamSynchronize(d.copy));
-  CIR_HIP(hipStreamSynchronize(d.chain));
+  if (d.chain) CIR_HIP(hipStreamSynchronize(d.chain));
   step("first uploads");
   return CIR_OK;
 }
 
 // Open the given devices, one host thread each (a device's warm-up waits on
 // its own streams only); the first failure in device order is returned.
-static int init_devices(std::vector<std::unique_ptr<Device>>& devs, uint64_t staging, bool lazy) {
+static int init_devices(std::vector<std::unique_ptr<Device>>& devs, uint64_t staging, bool lazy,
+                        bool one_shot) {
   if (devs.size() == 1) {
     DeviceGuard guard;
-    return init_device(*devs[0], staging, lazy);
+    return init_device(*devs[0], staging, lazy, one_shot);
   }
   std::vector<int> rc(devs.size(), 0);
   std::vector<std::string> err(devs.size());
   std::vector<std::thread> th;
   for (size_t i = 0; i < devs.size(); ++i)
     th.emplace_back([&, i] {
-      rc[i] = init_device(*devs[i], staging, lazy);
+      rc[i] = init_device(*devs[i], staging, lazy, one_shot);
       if (rc[i]) err[i] = t_last_error;
     });
   for (auto& t : th) t.join();
@@ -868,13 +876,14 @@ uint32_t cir_devices_for_bytes(uint64_t work_bytes, uint64_t staging_bytes, uint
 }
 
 int cir_init(cir_ctx** out, uint32_t device_mask, uint64_t staging_bytes) {
-  return cir_init_n(out, device_mask, staging_bytes, 0);
+  return cir_init_n(out, device_mask, staging_bytes, 0, 0);
 }
 
 int cir_init_n(cir_ctx** out, uint32_t device_mask, uint64_t staging_bytes,
-               uint32_t max_devices) {
+               uint32_t max_devices, uint32_t flags) {
   if (!out) return fail(CIR_EINVAL, "cir_init: null ctx");
   *out = nullptr;
+  if (flags & ~CIR_INIT_ONE_SHOT) return fail(CIR_EINVAL, "cir_init_n: unknown flags");
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);
   if (e != hipSuccess || n == 0)
@@ -908,7 +917,7 @@ int cir_init_n(cir_ctx** out, uint32_t device_mask, uint64_t staging_bytes,
   // the device-count hint: the first max_devices device states (distinct
   // GPUs first, CIR_DEBUG_SPLIT's extra states after them)
   if (max_devices && ctx->devs.size() > max_devices) ctx->devs.resize(max_devices);
-  int rc = init_devices(ctx->devs, ctx->staging, lazy);
+  int rc = init_devices(ctx->devs, ctx->staging, lazy, (flags & CIR_INIT_ONE_SHOT) != 0);
   if (rc) return rc;
   if (const char* v = std::getenv("CIR_FOOTER"))
     ctx->footer = strcmp(v, "gpu") == 0 ? CIR_FOOTER_GPU : CIR_FOOTER_HOST;

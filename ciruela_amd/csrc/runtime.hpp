@@ -116,7 +116,7 @@ ssize_t pread_staged(int fd, uint8_t* dst, size_t n, off_t off, bool nt);
 struct Device {
   int id = 0;
   hipStream_t compute = nullptr;
-  hipStream_t copy = nullptr;
+  hipStream_t copy = nullptr;  // == compute in a CIR_INIT_ONE_SHOT context
   // per-batch timing of the staged path (slot_submit records t_* events)
   bool record_times = false;
   hipEvent_t t_ref = nullptr;  // a scan's time origin on the copy stream

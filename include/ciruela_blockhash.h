@@ -101,8 +101,21 @@ int cir_init(cir_ctx** ctx, uint32_t device_mask, uint64_t staging_bytes);
 /* cir_init with a device-count hint: opens at most max_devices of the
  * devices device_mask selects, the lowest-numbered first (0 = no cap, as
  * cir_init).  With cir_devices_for_bytes a caller that knows how much input
- * it will stage opens only the devices that input can use. */
-int cir_init_n(cir_ctx** ctx, uint32_t device_mask, uint64_t staging_bytes, uint32_t max_devices);
+ * it will stage opens only the devices that input can use.  flags: 0 or
+ * CIR_INIT_ONE_SHOT. */
+int cir_init_n(cir_ctx** ctx, uint32_t device_mask, uint64_t staging_bytes, uint32_t max_devices,
+               uint32_t flags);
+/* A context for one short job (the CLI's sync of an input that fits one
+ * staging slot): each device gets ONE stream for its uploads and kernels and
+ * one staging slot.  A HIP stream on a hardware queue of its own costs 8-10
+ * ms to create in a fresh process (the first 19 ms; profiles/r05/
+ * start_env.log), and the copy, footer-chain and quad-part streams were
+ * ~25 ms of a 55 ms cir_init.  Every entry point still works: the other
+ * slots are allocated and the footer-chain stream created if a call needs
+ * them, uploads wait for the previous batch's kernels, and an ordered
+ * batch's quad part runs behind its lane part instead of beside it (config
+ * 3's mixed batch takes the sum of the two parts, not the longer). */
+#define CIR_INIT_ONE_SHOT 1u
 /* The devices worth opening for work_bytes of host-path input (a scan's
  * tree, a hash_file / hash_memory input): ceil(work_bytes / (2 x staging))
  * -- each device gets at least two staging batches, so its start-up and

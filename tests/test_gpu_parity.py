@@ -632,6 +632,40 @@ def test_context_device_hint(gpu, monkeypatch):
     c0.close()
 
 
+def test_one_shot_context(gpu, oracle, tmp_path):
+    """CIR_INIT_ONE_SHOT (the CLI's context for a small input): one stream
+    and one staging slot.  Every path still runs and matches the oracle: a
+    config-3-shaped descriptor batch and an exclusive-quad batch (the quad
+    part behind the lane part on the one stream, no relay), a ragged file on
+    the device, host batches over several slots (allocated on demand), a scan
+    with the GPU footer (its chain stream created on demand) and verify."""
+    c = gpu.Context(device_mask=1, staging_bytes=1 << 20, one_shot=True)
+    test_desc_mixed_ragged_shuffled(gpu, c, oracle)
+    test_desc_large_batch_exclusive_quad(gpu, c, oracle)
+    test_chunks_dev_vs_oracle(gpu, c, oracle, 32768, 32768 * 4099 + 77)
+    rng = random.Random(0x1D)
+    arena = rng.randbytes(5 << 20)
+    offs = list(range(0, len(arena) - 32768, 32768))
+    lens = [32768 - (i % 3) for i in range(len(offs))]
+    want = b"".join(oracle_digest(oracle, arena[o:o + ln]) for o, ln in zip(offs, lens))
+    assert c.hash_blocks(arena, offs, lens) == want
+    assert c.hash_memory(arena, 4096) == b"".join(
+        oracle_digest(oracle, arena[i:i + 4096]) for i in range(0, len(arena), 4096))
+    exp = bytearray(want)
+    exp[32 * 7] ^= 1
+    assert c.verify_blocks(arena, offs, lens, bytes(exp)) == [i != 7 for i in range(len(offs))]
+    t = c.verify_submit(arena[:32768], want[:32])
+    assert c.verify_wait(t) is True
+    root = tmp_path / "tree"
+    make_tree(root)
+    for mode in (c.FOOTER_GPU, c.FOOTER_HOST):
+        c.set_footer_mode(mode)
+        cfg = gpu.ScannerConfig.new().block_size(32768)
+        cfg.add_dir(str(root), "/")
+        assert gpu.v1.scan(cfg, context=c) == dirsig_oracle.scan(str(root), 32768, "blake2b/256")
+    c.close()
+
+
 def test_sha512_256_single_and_batches(gpu, ctx, oracle):
     """dir-signature's second hash type on the GPU vs the oracle."""
     import torch
@@ -1897,8 +1931,8 @@ def random_tree(root, rng, bs):
 def scan_case(gpu, seed, tmp_path, monkeypatch):
     """One randomized end-to-end scan against the scan oracle, over the
     scan's knobs: block size (up to one above the staging size), hash type,
-    reader threads, staging size (one not a multiple of 16), the
-    staging copy mode, the footer's placement, a split over 1-3 device
+    reader threads, staging size (one not a multiple of 16), a one-shot
+    context (one stream, slots on demand) or not, the staging copy mode, the footer's placement, a split over 1-3 device
     states (CIR_DEBUG_SPLIT on the one GPU) with stripes of 1-5 blocks or the
     default, and the index returned whole or written out as it goes."""
     rng = random.Random(seed)
@@ -1916,9 +1950,12 @@ def scan_case(gpu, seed, tmp_path, monkeypatch):
         # the scan deals stripes of blocks round-robin to the devices: make
         # them a few blocks long so small trees cross many stripe edges
         monkeypatch.setenv("CIR_DEBUG_STRIPE_BLOCKS", str(rng.choice([0, 1, 2, 5])))
+    # (drawn apart from rng, so the other draws of a seed stay as they were)
+    one_shot = random.Random(seed ^ 0x1D).random() < 0.3
     try:
         ctx = gpu.Context(device_mask=1,
-                          staging_bytes=rng.choice([1 << 20, 1000003, 3 << 20, 16 << 20]))
+                          staging_bytes=rng.choice([1 << 20, 1000003, 3 << 20, 16 << 20]),
+                          one_shot=one_shot)
     finally:
         monkeypatch.delenv("CIR_DEBUG_SPLIT", raising=False)
     ctx.set_footer_mode(rng.choice([ctx.FOOTER_HOST, ctx.FOOTER_GPU]))
@@ -1933,7 +1970,7 @@ def scan_case(gpu, seed, tmp_path, monkeypatch):
         got = gpu.v1.scan(cfg, context=ctx)
     monkeypatch.delenv("CIR_DEBUG_STRIPE_BLOCKS", raising=False)
     want = dirsig_oracle.scan(str(root), bs, hash_name)
-    assert got == want, (seed, bs, hash_name, split)
+    assert got == want, (seed, bs, hash_name, split, one_shot)
     assert gpu.get_hash(got) == gpu.get_hash(want)
     ctx.close()
 
@@ -2173,7 +2210,7 @@ def test_verify_async_forget_and_expiry(gpu, oracle):
 def host_case(gpu, oracle, seed, tmp_path, monkeypatch):
     """One randomized round of the host-memory entry points against the
     oracle, over the staging knobs: staging size, copy mode, 1-3 device
-    states.  Descriptor batches (cir_hash_blocks, both hash types), batch
+    states, a one-shot context or not.  Descriptor batches (cir_hash_blocks, both hash types), batch
     and asynchronous verify with some wrong digests, an in-memory file
     (cir_hash_memory) and a file read from an offset (cir_hash_file)."""
     rng = random.Random(seed)
@@ -2181,9 +2218,11 @@ def host_case(gpu, oracle, seed, tmp_path, monkeypatch):
     split = rng.choice([1, 1, 2, 3])
     if split > 1:
         monkeypatch.setenv("CIR_DEBUG_SPLIT", str(split))
+    one_shot = random.Random(seed ^ 0x1D).random() < 0.3
     try:
         c = gpu.Context(device_mask=1,
-                        staging_bytes=rng.choice([1 << 20, 1000003, 5 << 20, 32 << 20]))
+                        staging_bytes=rng.choice([1 << 20, 1000003, 5 << 20, 32 << 20]),
+                        one_shot=one_shot)
     finally:
         monkeypatch.delenv("CIR_DEBUG_SPLIT", raising=False)
     arena = rng.randbytes(rng.choice([1 << 16, 3 << 20, 9 << 20]))
