@@ -15,6 +15,7 @@
 //                      [--replace SRC:/DEST[:OLD_IMAGE_ID]] ...
 //   ciruela-index hash [--block-size N] FILE...   (per-block BlockHash list)
 #include <dirent.h>
+#include <errno.h>
 #include <fcntl.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -143,8 +144,23 @@ int main(int argc, char** argv) {
       }
       return argv[++i];
     };
-    if (a == "--disk-threads") threads = (uint32_t)std::stoul(val());
-    else if (a == "--block-size") bs = std::stoull(val());
+    if (a == "--disk-threads" || a == "--block-size") {
+      // a decimal count (clap's usize parse in the reference): anything else
+      // is a usage error, not an exception out of main
+      const std::string v = val();
+      char* end = nullptr;
+      errno = 0;
+      const unsigned long long n = strtoull(v.c_str(), &end, 10);
+      if (v.empty() || v[0] == '-' || *end || errno ||
+          (a == "--disk-threads" && n > 0xffffffffull)) {
+        fprintf(stderr, "invalid value for %s: %s\n", a.c_str(), v.c_str());
+        return 2;
+      }
+      if (a == "--disk-threads")
+        threads = (uint32_t)n;
+      else
+        bs = n;
+    }
     else if (a == "--index-dir") index_dir = val();
     else if (a == "--append" || a == "--append-weak" || a == "--replace") {
       Job j;

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <memory>
+#include <new>
 #include <shared_mutex>
 #include <unordered_map>
 
@@ -54,12 +55,14 @@ using namespace cir;
 extern "C" {
 
 
-cir_indexes* cir_indexes_new(void) { return reinterpret_cast<cir_indexes*>(new IndexMap()); }
+cir_indexes* cir_indexes_new(void) {
+  return reinterpret_cast<cir_indexes*>(new (std::nothrow) IndexMap());  // NULL: no memory
+}
 void cir_indexes_free(cir_indexes* h) { delete reinterpret_cast<IndexMap*>(h); }
 
 // InMemoryIndexes::register_index (src/index.rs:98-105)
 int cir_indexes_register(cir_indexes* h, const uint8_t* data, size_t len, uint8_t* id_out,
-                         size_t* id_len) {
+                         size_t* id_len) try {
   if (!h || !data || !id_out || !id_len) return fail(CIR_EINVAL, "null pointer");
   std::vector<uint8_t> id;
   std::string err;
@@ -74,11 +77,11 @@ int cir_indexes_register(cir_indexes* h, const uint8_t* data, size_t len, uint8_
   memcpy(id_out, id.data(), id.size());
   *id_len = id.size();
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
 // GetIndex::read_index (src/index.rs:106-123)
 int cir_indexes_read(cir_indexes* h, const uint8_t* id, size_t id_len, uint8_t** data_out,
-                     size_t* len_out) {
+                     size_t* len_out) try {
   if (!h || !id || !data_out || !len_out) return fail(CIR_EINVAL, "null pointer");
   auto* m = reinterpret_cast<IndexMap*>(h);
   std::shared_ptr<std::string> v;
@@ -94,9 +97,11 @@ int cir_indexes_read(cir_indexes* h, const uint8_t* id, size_t id_len, uint8_t**
   memcpy(*data_out, v->data(), v->size());
   *len_out = v->size();
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
-cir_blocks* cir_blocks_new(void) { return reinterpret_cast<cir_blocks*>(new BlockMap()); }
+cir_blocks* cir_blocks_new(void) {
+  return reinterpret_cast<cir_blocks*>(new (std::nothrow) BlockMap());  // NULL: no memory
+}
 void cir_blocks_free(cir_blocks* h) { delete reinterpret_cast<BlockMap*>(h); }
 
 size_t cir_blocks_len(cir_blocks* h) {
@@ -107,7 +112,7 @@ size_t cir_blocks_len(cir_blocks* h) {
 
 // ThreadedBlockReader::register_dir (src/blocks.rs:145-183): every block of
 // every file in the index -> Disk{dir + path, idx * bs, min(left, bs)}.
-int cir_blocks_register_dir(cir_blocks* h, const char* dir, const uint8_t* index, size_t len) {
+int cir_blocks_register_dir(cir_blocks* h, const char* dir, const uint8_t* index, size_t len) try {
   if (!h || !dir || !index) return fail(CIR_EINVAL, "null pointer");
   dirsig::Index idx;
   std::string err;
@@ -138,7 +143,7 @@ int cir_blocks_register_dir(cir_blocks* h, const char* dir, const uint8_t* index
     }
   }
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
 // ThreadedBlockReader::register_memory_blocks (src/blocks.rs:187-204): hash
 // `data` in block_size blocks (on the GPU) and serve them from memory.
@@ -150,7 +155,7 @@ int cir_blocks_register_dir(cir_blocks* h, const char* dir, const uint8_t* index
 // src/client/put_file/network.rs:56): every block id is
 // Hashes::hash_file(hash_type, ..)'s digest of the block.
 int cir_blocks_register_memory_ht(cir_ctx* ctx, cir_blocks* h, int hash_type, const uint8_t* data,
-                                  size_t len, uint64_t block_size) {
+                                  size_t len, uint64_t block_size) try {
   if (!ctx || !h || (len && !data)) return fail(CIR_EINVAL, "null pointer");
   if (!valid_hash_type(hash_type)) return fail(CIR_EINVAL, "unknown hash type");
   uint8_t* hashes = nullptr;
@@ -171,17 +176,17 @@ int cir_blocks_register_memory_ht(cir_ctx* ctx, cir_blocks* h, int hash_type, co
   }
   free(hashes);
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
 int cir_blocks_register_memory(cir_ctx* ctx, cir_blocks* h, const uint8_t* data, size_t len,
-                               uint64_t block_size) {
+                               uint64_t block_size) try {
   return cir_blocks_register_memory_ht(ctx, h, CIR_HASH_BLAKE2B_256, data, len, block_size);
-}
+} CIR_CATCH_BOUNDARY
 
 // GetBlock::read_block (src/blocks.rs:207-240).  Unlike the reference's
 // single read() + assert_eq! (:227-231), short reads are retried; a file that
 // is shorter than recorded is an I/O error, not a panic.
-int cir_blocks_read(cir_blocks* h, const uint8_t hash[32], uint8_t** data_out, size_t* len_out) {
+int cir_blocks_read(cir_blocks* h, const uint8_t hash[32], uint8_t** data_out, size_t* len_out) try {
   if (!h || !hash || !data_out || !len_out) return fail(CIR_EINVAL, "null pointer");
   auto* m = reinterpret_cast<BlockMap*>(h);
   BlockPtr p;
@@ -220,6 +225,6 @@ int cir_blocks_read(cir_blocks* h, const uint8_t hash[32], uint8_t** data_out, s
   *data_out = out;
   *len_out = p.size;
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
 }  // extern "C"

@@ -20,6 +20,8 @@
 #include <condition_variable>
 #include <cstdlib>
 #include <deque>
+#include <new>
+#include <system_error>
 #include <thread>
 #include <unordered_map>
 
@@ -29,6 +31,28 @@ static thread_local std::string t_last_error;
 
 int fail(int code, const std::string& msg) {
   t_last_error = msg;
+  return code;
+}
+
+int boundary_error() noexcept {
+  int code = CIR_EIO;
+  const char* what = "unknown exception";
+  try {
+    throw;  // the exception being handled by the entry point's catch (...)
+  } catch (const std::bad_alloc& e) {
+    code = CIR_ENOMEM;
+    what = e.what();
+  } catch (const std::system_error& e) {
+    if (e.code() == std::errc::resource_unavailable_try_again) code = CIR_ENOMEM;
+    what = e.what();
+  } catch (const std::exception& e) {
+    what = e.what();
+  } catch (...) {
+  }
+  try {
+    t_last_error = std::string("C++ exception in the library: ") + what;
+  } catch (...) {
+  }
   return code;
 }
 
@@ -858,11 +882,11 @@ using namespace cir;
 
 extern "C" {
 
-int cir_device_count(void) {
+int cir_device_count(void) try {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
   return n;
-}
+} CIR_CATCH_BOUNDARY
 
 uint32_t cir_devices_for_bytes(uint64_t work_bytes, uint64_t staging_bytes, uint32_t visible) {
   if (visible == 0) return 0;
@@ -875,12 +899,12 @@ uint32_t cir_devices_for_bytes(uint64_t work_bytes, uint64_t staging_bytes, uint
   return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n, visible));
 }
 
-int cir_init(cir_ctx** out, uint32_t device_mask, uint64_t staging_bytes) {
+int cir_init(cir_ctx** out, uint32_t device_mask, uint64_t staging_bytes) try {
   return cir_init_n(out, device_mask, staging_bytes, 0, 0);
-}
+} CIR_CATCH_BOUNDARY
 
 int cir_init_n(cir_ctx** out, uint32_t device_mask, uint64_t staging_bytes,
-               uint32_t max_devices, uint32_t flags) {
+               uint32_t max_devices, uint32_t flags) try {
   if (!out) return fail(CIR_EINVAL, "cir_init: null ctx");
   *out = nullptr;
   if (flags & ~CIR_INIT_ONE_SHOT) return fail(CIR_EINVAL, "cir_init_n: unknown flags");
@@ -923,16 +947,16 @@ int cir_init_n(cir_ctx** out, uint32_t device_mask, uint64_t staging_bytes,
     ctx->footer = strcmp(v, "gpu") == 0 ? CIR_FOOTER_GPU : CIR_FOOTER_HOST;
   *out = ctx.release();
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
 void cir_destroy(cir_ctx* ctx) { delete ctx; }
 
-int cir_ctx_devices(const cir_ctx* ctx, int* ids, int max_ids) {
+int cir_ctx_devices(const cir_ctx* ctx, int* ids, int max_ids) try {
   if (!ctx) return fail(CIR_EINVAL, "null ctx");
   int n = (int)ctx->devs.size();
   for (int i = 0; i < n && i < max_ids; ++i) ids[i] = ctx->devs[i]->id;
   return n;
-}
+} CIR_CATCH_BOUNDARY
 
 const char* cir_strerror(int status) {
   switch (status) {
@@ -956,7 +980,7 @@ const char* cir_last_error(void) { return t_last_error.c_str(); }
 void cir_free(void* p) { free(p); }
 
 int cir_hash_chunks_dev(cir_ctx* ctx, const void* d_data, uint64_t nbytes, uint64_t block_size,
-                        uint8_t* d_out, void* stream) {
+                        uint8_t* d_out, void* stream) try {
   if (block_size == 0) return fail(CIR_EINVAL, "block_size must be > 0");
   if (nbytes && (!d_data || !d_out)) return fail(CIR_EINVAL, "null device pointer");
   if (reinterpret_cast<uintptr_t>(d_out) & 15u)
@@ -977,11 +1001,11 @@ int cir_hash_chunks_dev(cir_ctx* ctx, const void* d_data, uint64_t nbytes, uint6
   }
   CIR_HIP(dev::launch_chunks((const uint8_t*)d_data, nbytes, block_size, d_out, s));
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
 int cir_hash_blocks_dev_ht(cir_ctx* ctx, int hash_type, const void* d_arena,
                            const uint64_t* d_off, const uint32_t* d_len, size_t nblk,
-                           uint8_t* d_out, void* stream) {
+                           uint8_t* d_out, void* stream) try {
   if (!valid_hash_type(hash_type)) return fail(CIR_EINVAL, "unknown hash type");
   if (nblk && (!d_arena || !d_off || !d_len || !d_out))
     return fail(CIR_EINVAL, "null device pointer");
@@ -1004,16 +1028,16 @@ int cir_hash_blocks_dev_ht(cir_ctx* ctx, int hash_type, const void* d_arena,
   else
     CIR_HIP(dev::launch_general_desc((const uint8_t*)d_arena, d_off, d_len, nullptr, nblk, d_out, s));
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
 int cir_hash_blocks_dev(cir_ctx* ctx, const void* d_arena, const uint64_t* d_off,
-                        const uint32_t* d_len, size_t nblk, uint8_t* d_out, void* stream) {
+                        const uint32_t* d_len, size_t nblk, uint8_t* d_out, void* stream) try {
   return cir_hash_blocks_dev_ht(ctx, CIR_HASH_BLAKE2B_256, d_arena, d_off, d_len, nblk, d_out,
                                 stream);
-}
+} CIR_CATCH_BOUNDARY
 
 int cir_hash_blocks_ht(cir_ctx* ctx, int hash_type, const uint8_t* h_arena, const uint64_t* off,
-                       const uint32_t* len, size_t nblk, uint8_t* h_out) {
+                       const uint32_t* len, size_t nblk, uint8_t* h_out) try {
   if (!ctx) return fail(CIR_EINVAL, "null ctx");
   if (!valid_hash_type(hash_type)) return fail(CIR_EINVAL, "unknown hash type");
   if (nblk == 0) return CIR_OK;
@@ -1034,12 +1058,12 @@ int cir_hash_blocks_ht(cir_ctx* ctx, int hash_type, const uint8_t* h_arena, cons
     if (i >= nd || cut[i] >= cut[i + 1]) return (int)CIR_OK;
     return run_blocks(ctx, d, h_arena, off, len, cut[i], cut[i + 1], h_out, hash_type);
   });
-}
+} CIR_CATCH_BOUNDARY
 
 int cir_hash_blocks(cir_ctx* ctx, const uint8_t* h_arena, const uint64_t* off,
-                    const uint32_t* len, size_t nblk, uint8_t* h_out) {
+                    const uint32_t* len, size_t nblk, uint8_t* h_out) try {
   return cir_hash_blocks_ht(ctx, CIR_HASH_BLAKE2B_256, h_arena, off, len, nblk, h_out);
-}
+} CIR_CATCH_BOUNDARY
 
 // Inputs up to this size take the one-launch path (k_single): the chain of
 // a larger input runs for milliseconds, so the staged path's fixed cost no
@@ -1238,16 +1262,16 @@ static int single_shot(int ht, const uint8_t* p, size_t n, uint8_t* out) {
   return cir_hash_blocks_ht(ctx, ht, n ? p : &empty, &off, &len, 1, out);
 }
 
-int cir_blake2b256(const uint8_t* p, size_t n, uint8_t out[CIR_DIGEST_BYTES]) {
+int cir_blake2b256(const uint8_t* p, size_t n, uint8_t out[CIR_DIGEST_BYTES]) try {
   return single_shot(CIR_HASH_BLAKE2B_256, p, n, out);
-}
+} CIR_CATCH_BOUNDARY
 
-int cir_sha512_256(const uint8_t* p, size_t n, uint8_t out[CIR_DIGEST_BYTES]) {
+int cir_sha512_256(const uint8_t* p, size_t n, uint8_t out[CIR_DIGEST_BYTES]) try {
   return single_shot(CIR_HASH_SHA512_256, p, n, out);
-}
+} CIR_CATCH_BOUNDARY
 
 int cir_hash_file_ht(cir_ctx* ctx, int hash_type, int fd, uint64_t block_size,
-                     uint64_t* size_out, uint8_t** hashes_out, size_t* nhash_out) {
+                     uint64_t* size_out, uint8_t** hashes_out, size_t* nhash_out) try {
   if (!ctx || !size_out || !hashes_out || !nhash_out) return fail(CIR_EINVAL, "null pointer");
   if (block_size == 0 || block_size > 0xffffffffull)
     return fail(CIR_EINVAL, "block_size must be in 1 .. 2^32-1");
@@ -1329,16 +1353,16 @@ int cir_hash_file_ht(cir_ctx* ctx, int hash_type, int fd, uint64_t block_size,
   int rc = run_file(ctx, rd, block_size, size_out, h, hash_type, known);
   if (rc) return rc;
   return export_hashes(h, hashes_out, nhash_out);
-}
+} CIR_CATCH_BOUNDARY
 
 int cir_hash_file(cir_ctx* ctx, int fd, uint64_t block_size, uint64_t* size_out,
-                  uint8_t** hashes_out, size_t* nhash_out) {
+                  uint8_t** hashes_out, size_t* nhash_out) try {
   return cir_hash_file_ht(ctx, CIR_HASH_BLAKE2B_256, fd, block_size, size_out, hashes_out,
                           nhash_out);
-}
+} CIR_CATCH_BOUNDARY
 
 int cir_hash_memory_ht(cir_ctx* ctx, int hash_type, const uint8_t* data, uint64_t size,
-                       uint64_t block_size, uint8_t** hashes_out, size_t* nhash_out) {
+                       uint64_t block_size, uint8_t** hashes_out, size_t* nhash_out) try {
   if (!ctx || !hashes_out || !nhash_out || (size && !data)) return fail(CIR_EINVAL, "null pointer");
   if (block_size == 0 || block_size > 0xffffffffull)
     return fail(CIR_EINVAL, "block_size must be in 1 .. 2^32-1");
@@ -1372,19 +1396,19 @@ int cir_hash_memory_ht(cir_ctx* ctx, int hash_type, const uint8_t* data, uint64_
   int rc = run_file(ctx, rd, block_size, &got_size, h, hash_type, size, /*exact=*/true);
   if (rc) return rc;
   return export_hashes(h, hashes_out, nhash_out);
-}
+} CIR_CATCH_BOUNDARY
 
 int cir_hash_memory(cir_ctx* ctx, const uint8_t* data, uint64_t size, uint64_t block_size,
-                    uint8_t** hashes_out, size_t* nhash_out) {
+                    uint8_t** hashes_out, size_t* nhash_out) try {
   return cir_hash_memory_ht(ctx, CIR_HASH_BLAKE2B_256, data, size, block_size, hashes_out,
                             nhash_out);
-}
+} CIR_CATCH_BOUNDARY
 
 // ---- verification (row f2) ---------------------------------------------
 
 int cir_verify_blocks_dev(cir_ctx* ctx, int hash_type, const void* d_arena, const uint64_t* d_off,
                           const uint32_t* d_len, size_t nblk, const uint8_t* d_expected,
-                          uint8_t* d_digests, uint8_t* d_ok, uint32_t* d_nbad, void* stream) {
+                          uint8_t* d_digests, uint8_t* d_ok, uint32_t* d_nbad, void* stream) try {
   if (nblk && (!d_expected || !d_digests)) return fail(CIR_EINVAL, "null device pointer");
   if ((reinterpret_cast<uintptr_t>(d_expected) | reinterpret_cast<uintptr_t>(d_digests)) & 15u)
     return fail(CIR_EINVAL, "digest arrays must be 16-byte aligned");
@@ -1394,11 +1418,11 @@ int cir_verify_blocks_dev(cir_ctx* ctx, int hash_type, const void* d_arena, cons
   if (rc) return rc;
   CIR_HIP(dev::launch_verify(d_digests, d_expected, nblk, d_ok, d_nbad, s));
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
 int cir_verify_blocks(cir_ctx* ctx, int hash_type, const uint8_t* h_arena, const uint64_t* off,
                       const uint32_t* len, size_t nblk, const uint8_t* expected, uint8_t* ok_out,
-                      size_t* nbad_out) {
+                      size_t* nbad_out) try {
   if (nblk && !expected) return fail(CIR_EINVAL, "null pointer");
   std::vector<uint8_t> got(nblk * 32);
   int rc = cir_hash_blocks_ht(ctx, hash_type, h_arena, off, len, nblk, got.data());
@@ -1411,7 +1435,7 @@ int cir_verify_blocks(cir_ctx* ctx, int hash_type, const uint8_t* h_arena, const
   }
   if (nbad_out) *nbad_out = nbad;
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
 }  // extern "C"
 
@@ -1439,61 +1463,61 @@ static VerifyQueue* verify_queue(cir_ctx* ctx) {
 extern "C" {
 
 int cir_verify_submit(cir_ctx* ctx, int hash_type, const uint8_t* data, size_t n,
-                      const uint8_t expected[CIR_DIGEST_BYTES], uint64_t* ticket) {
+                      const uint8_t expected[CIR_DIGEST_BYTES], uint64_t* ticket) try {
   if (!ctx || !ticket || !expected || (n && !data)) return fail(CIR_EINVAL, "null pointer");
   if (!valid_hash_type(hash_type)) return fail(CIR_EINVAL, "unknown hash type");
   if (n > 0xffffffffull) return fail(CIR_EINVAL, "block longer than 4 GiB");
   std::string err;
   const int rc = verify_queue(ctx)->submit(hash_type, data, n, expected, ticket, &err);
   return rc ? fail(rc, err) : CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
-int cir_verify_poll(cir_ctx* ctx, uint64_t ticket, int* state) {
+int cir_verify_poll(cir_ctx* ctx, uint64_t ticket, int* state) try {
   if (!ctx || !state) return fail(CIR_EINVAL, "null pointer");
   std::string err;
   const int v = verify_queue(ctx)->poll(ticket, &err);
   if (v < 0) return fail(v, err);
   *state = v;
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
-int cir_verify_wait(cir_ctx* ctx, uint64_t ticket, int* ok) {
+int cir_verify_wait(cir_ctx* ctx, uint64_t ticket, int* ok) try {
   if (!ctx || !ok) return fail(CIR_EINVAL, "null pointer");
   std::string err;
   const int v = verify_queue(ctx)->wait(ticket, &err);
   if (v < 0) return fail(v, err);
   *ok = v == 1;
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
-int cir_verify_forget(cir_ctx* ctx, uint64_t ticket) {
+int cir_verify_forget(cir_ctx* ctx, uint64_t ticket) try {
   if (!ctx) return fail(CIR_EINVAL, "null ctx");
   std::string err;
   const int rc = verify_queue(ctx)->forget(ticket, &err);
   return rc ? fail(rc, err) : CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
-int cir_verify_window(cir_ctx* ctx, uint32_t window_us, uint32_t max_batch) {
+int cir_verify_window(cir_ctx* ctx, uint32_t window_us, uint32_t max_batch) try {
   if (!ctx || max_batch == 0) return fail(CIR_EINVAL, "bad argument");
   verify_queue(ctx)->window(window_us, max_batch);
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
-int cir_verify_limits(cir_ctx* ctx, uint64_t max_bytes, uint64_t max_results, int flags) {
+int cir_verify_limits(cir_ctx* ctx, uint64_t max_bytes, uint64_t max_results, int flags) try {
   if (!ctx) return fail(CIR_EINVAL, "null ctx");
   if (flags & ~CIR_VERIFY_NONBLOCK) return fail(CIR_EINVAL, "unknown flags");
   verify_queue(ctx)->limits(max_bytes, max_results, (flags & CIR_VERIFY_NONBLOCK) != 0);
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
-int cir_verify_stats(cir_ctx* ctx, uint64_t out[CIR_VERIFY_STATS_FIELDS]) {
+int cir_verify_stats(cir_ctx* ctx, uint64_t out[CIR_VERIFY_STATS_FIELDS]) try {
   if (!ctx || !out) return fail(CIR_EINVAL, "null pointer");
   verify_queue(ctx)->stats(out);
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
 int cir_check_file(cir_ctx* ctx, int hash_type, int fd, uint64_t block_size,
-                   const uint8_t* expected, size_t nhash, int* ok_out) {
+                   const uint8_t* expected, size_t nhash, int* ok_out) try {
   if (!ctx || !ok_out || (nhash && !expected)) return fail(CIR_EINVAL, "null pointer");
   uint8_t* h = nullptr;
   size_t n = 0;
@@ -1503,35 +1527,35 @@ int cir_check_file(cir_ctx* ctx, int hash_type, int fd, uint64_t block_size,
   *ok_out = n == nhash && (n == 0 || memcmp(h, expected, 32 * n) == 0);
   free(h);
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
 int cir_debug_hash_uniform_dev(int loader, const void* d_data, uint64_t block_size, uint64_t nblk,
-                               uint8_t* d_out, void* stream) {
+                               uint8_t* d_out, void* stream) try {
   if (block_size == 0 || block_size % 128 || nblk % dev::kThreads || (loader != 0 && loader != 1) ||
       (reinterpret_cast<uintptr_t>(d_data) & 15u))
     return fail(CIR_EINVAL, "uniform kernel needs bs % 128 == 0, nblk % 256 == 0, 16-B alignment");
   CIR_HIP(dev::launch_uniform(loader == 0 ? dev::Loader::kGlds : dev::Loader::kDirect,
                               (const uint8_t*)d_data, block_size, nblk, d_out, (hipStream_t)stream));
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
-int cir_debug_compress_only_dev(uint64_t nlanes, uint32_t lines, uint8_t* d_out, void* stream) {
+int cir_debug_compress_only_dev(uint64_t nlanes, uint32_t lines, uint8_t* d_out, void* stream) try {
   if (nlanes % dev::kThreads || lines == 0 || !d_out)
     return fail(CIR_EINVAL, "compress-only kernel needs nlanes % 256 == 0, lines > 0, an output");
   CIR_HIP(dev::launch_compress_only(nlanes, lines, d_out, (hipStream_t)stream));
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
-int cir_debug_desc_timing(cir_ctx* ctx, int enable) {
+int cir_debug_desc_timing(cir_ctx* ctx, int enable) try {
   if (!ctx || ctx->devs.empty()) return fail(CIR_EINVAL, "null ctx");
   Device& d = *ctx->devs[0];
   std::lock_guard<std::mutex> lk(d.order_mu);
   d.timing = enable != 0;
   d.tev_used = 0;
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
-int cir_debug_desc_times(cir_ctx* ctx, double out[5]) {
+int cir_debug_desc_times(cir_ctx* ctx, double out[5]) try {
   if (!ctx || ctx->devs.empty() || !out) return fail(CIR_EINVAL, "null pointer");
   Device& d = *ctx->devs[0];
   std::lock_guard<std::mutex> lk(d.order_mu);
@@ -1554,10 +1578,10 @@ int cir_debug_desc_times(cir_ctx* ctx, double out[5]) {
     out[4] += std::max(to_q, to_l);
   }
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
 int cir_debug_device_identity(int device, char* pci_bus_id, size_t len, uint8_t uuid[16],
-                              uint64_t clocks[5]) {
+                              uint64_t clocks[5]) try {
   if (!pci_bus_id || len < 13 || !uuid || !clocks) return fail(CIR_EINVAL, "null pointer");
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
@@ -1580,19 +1604,19 @@ int cir_debug_device_identity(int device, char* pci_bus_id, size_t len, uint8_t 
   if (e != hipSuccess) return hip_fail(e, "clock probe");
   clocks[4] = (uint64_t)rate_khz;
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
 uint64_t cir_debug_relay_blocks(uint64_t nfull, uint64_t block_size) {
   return dev::relay_blocks(nfull, block_size);
 }
 
 int cir_fill_splitmix64_dev(void* d_ptr, uint64_t nbytes, uint64_t seed, uint64_t block_bytes,
-                            uint64_t first_block, void* stream) {
+                            uint64_t first_block, void* stream) try {
   if (nbytes % 8 || block_bytes % 8) return fail(CIR_EINVAL, "sizes must be multiples of 8");
   if (nbytes && !d_ptr) return fail(CIR_EINVAL, "null device pointer");
   CIR_HIP(dev::launch_fill_splitmix64((uint64_t*)d_ptr, nbytes / 8, seed, block_bytes / 8,
                                       first_block, (hipStream_t)stream));
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
 }  // extern "C"

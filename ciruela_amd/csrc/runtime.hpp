@@ -22,6 +22,18 @@ namespace cir {
 int fail(int code, const std::string& msg);
 int hip_fail(hipError_t e, const char* what);
 
+// No C++ exception crosses the C ABI (a Rust caller unwinding through it is
+// undefined behaviour; a C caller would be terminated): every int-returning
+// entry point is a function-try-block ending in CIR_CATCH_BOUNDARY.  A failed
+// host allocation (std::bad_alloc) or a thread that could not start
+// (std::system_error, resource_unavailable_try_again) becomes CIR_ENOMEM,
+// anything else CIR_EIO, with the exception's text in cir_last_error.
+int boundary_error() noexcept;
+#define CIR_CATCH_BOUNDARY \
+  catch (...) {            \
+    return cir::boundary_error(); \
+  }
+
 #define CIR_HIP(expr)                                  \
   do {                                                 \
     hipError_t cir_e_ = (expr);                        \

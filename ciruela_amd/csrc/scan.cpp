@@ -847,22 +847,22 @@ extern "C" {
 
 int cir_scan_v1(cir_ctx* ctx, const char* const* dirs, const char* const* prefixes, size_t ndirs,
                 uint64_t block_size, int hash_type, uint32_t threads, uint8_t** index_out,
-                size_t* len_out) {
+                size_t* len_out) try {
   return scan_impl(ctx, dirs, prefixes, ndirs, block_size, hash_type, threads, nullptr, index_out,
                    len_out);
-}
+} CIR_CATCH_BOUNDARY
 
 int cir_scan_v1_write(cir_ctx* ctx, const char* const* dirs, const char* const* prefixes,
                       size_t ndirs, uint64_t block_size, int hash_type, uint32_t threads,
-                      cir_write_fn write, void* user, size_t* len_out) {
+                      cir_write_fn write, void* user, size_t* len_out) try {
   const IndexSink sink{write, user};
   return scan_impl(ctx, dirs, prefixes, ndirs, block_size, hash_type, threads, &sink, nullptr,
                    len_out);
-}
+} CIR_CATCH_BOUNDARY
 
 // RawIndex::into_mut + MutableIndex::to_raw_data: parse, rebuild the tree and
 // re-emit it in the reference's order with a freshly computed footer.
-int cir_index_rewrite(cir_ctx* ctx, const uint8_t* in, size_t len, uint8_t** out, size_t* out_len) {
+int cir_index_rewrite(cir_ctx* ctx, const uint8_t* in, size_t len, uint8_t** out, size_t* out_len) try {
   if (!in || !out || !out_len) return fail(CIR_EINVAL, "null pointer");
   dirsig::Index idx;
   std::string err;
@@ -929,16 +929,16 @@ int cir_index_rewrite(cir_ctx* ctx, const uint8_t* in, size_t len, uint8_t** out
   *out = em.finish_malloc(footer, 32, out_len);
   if (!*out) return fail(CIR_ENOMEM, "malloc");
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
-int cir_set_footer_mode(cir_ctx* ctx, int mode) {
+int cir_set_footer_mode(cir_ctx* ctx, int mode) try {
   if (!ctx) return fail(CIR_EINVAL, "null ctx");
   if (mode != CIR_FOOTER_HOST && mode != CIR_FOOTER_GPU) return fail(CIR_EINVAL, "unknown footer mode");
   ctx->footer = mode;
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
-int cir_debug_scan_timing(cir_ctx* ctx, int enable) {
+int cir_debug_scan_timing(cir_ctx* ctx, int enable) try {
   if (!ctx) return fail(CIR_EINVAL, "null ctx");
   std::lock_guard<std::mutex> sl(ctx->stats.mu);
   ctx->stats.on = enable != 0;
@@ -948,9 +948,9 @@ int cir_debug_scan_timing(cir_ctx* ctx, int enable) {
     ctx->stats.scans = 0;
   }
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
-int cir_debug_scan_batches(cir_ctx* ctx, double* rows, size_t max_rows, size_t* nrows) {
+int cir_debug_scan_batches(cir_ctx* ctx, double* rows, size_t max_rows, size_t* nrows) try {
   if (!ctx || !nrows || (max_rows && !rows)) return fail(CIR_EINVAL, "null pointer");
   std::lock_guard<std::mutex> sl(ctx->stats.mu);
   const auto& b = ctx->stats.batches;
@@ -958,34 +958,34 @@ int cir_debug_scan_batches(cir_ctx* ctx, double* rows, size_t max_rows, size_t* 
     memcpy(rows + i * kScanBatchFields, b[i].data(), sizeof(double) * kScanBatchFields);
   *nrows = b.size();
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
-int cir_debug_scan_phases(cir_ctx* ctx, double out[CIR_SCAN_PHASE_FIELDS]) {
+int cir_debug_scan_phases(cir_ctx* ctx, double out[CIR_SCAN_PHASE_FIELDS]) try {
   if (!ctx || !out) return fail(CIR_EINVAL, "null pointer");
   std::lock_guard<std::mutex> sl(ctx->stats.mu);
   memcpy(out, ctx->stats.phases.data(), sizeof(double) * kScanPhaseFields);
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
-int cir_debug_host_blake2b256(const uint8_t* p, size_t n, size_t piece, uint8_t out[32]) {
+int cir_debug_host_blake2b256(const uint8_t* p, size_t n, size_t piece, uint8_t out[32]) try {
   if (!out || (n && !p)) return fail(CIR_EINVAL, "null pointer");
   host::Blake2b256 h;
   if (piece == 0) piece = n;
   for (size_t off = 0; off < n; off += piece) h.update(p + off, std::min(piece, n - off));
   h.final(out);
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
-int cir_debug_host_sha512_256(const uint8_t* p, size_t n, size_t piece, uint8_t out[32]) {
+int cir_debug_host_sha512_256(const uint8_t* p, size_t n, size_t piece, uint8_t out[32]) try {
   if (!out || (n && !p)) return fail(CIR_EINVAL, "null pointer");
   host::Sha512_256 h;
   if (piece == 0) piece = n;
   for (size_t off = 0; off < n; off += piece) h.update(p + off, std::min(piece, n - off));
   h.final(out);
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
-int cir_index_get_hash(const uint8_t* index, size_t len, uint8_t* id_out, size_t* id_len) {
+int cir_index_get_hash(const uint8_t* index, size_t len, uint8_t* id_out, size_t* id_len) try {
   if (!index || !id_out || !id_len) return fail(CIR_EINVAL, "null pointer");
   std::vector<uint8_t> id;
   std::string err;
@@ -994,6 +994,6 @@ int cir_index_get_hash(const uint8_t* index, size_t len, uint8_t* id_out, size_t
   memcpy(id_out, id.data(), id.size());
   *id_len = id.size();
   return CIR_OK;
-}
+} CIR_CATCH_BOUNDARY
 
 }  // extern "C"

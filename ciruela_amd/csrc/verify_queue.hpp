@@ -35,6 +35,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <new>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -69,7 +70,8 @@ class VerifyQueue {
   VerifyQueue(const VerifyQueue&) = delete;
   VerifyQueue& operator=(const VerifyQueue&) = delete;
 
-  // 0 with *ticket, or CIR_EAGAIN (non-blocking, no room; *err says why)
+  // 0 with *ticket, CIR_EAGAIN (non-blocking, no room; *err says why) or
+  // CIR_ENOMEM (a new batch's arena could not be allocated)
   int submit(int ht, const uint8_t* data, size_t n, const uint8_t* expected, uint64_t* ticket,
              std::string* err) {
     std::unique_lock<std::mutex> lk(mu_);
@@ -105,7 +107,11 @@ class VerifyQueue {
       // one batch's arena: half the byte bound, so a batch can form while
       // the previous one is verified; a spare arena of a verified batch is
       // reused (its pages are already faulted in)
-      arena_for(*nb, std::max<uint64_t>(n, std::max<uint64_t>(1, max_bytes_ / 2)));
+      if (!arena_for(*nb, std::max<uint64_t>(n, std::max<uint64_t>(1, max_bytes_ / 2)))) {
+        *err = "verify batch arena of " + std::to_string(std::max<uint64_t>(n, max_bytes_ / 2)) +
+               " bytes";
+        return CIR_ENOMEM;
+      }
       nb->first = std::chrono::steady_clock::now();
       b = nb.get();
       queue_.push_back(std::move(nb));
@@ -237,18 +243,20 @@ class VerifyQueue {
     return r;
   }
 
-  // b gets an arena of at least `bytes`: a spare one when one is big enough
-  // (caller holds mu_)
-  void arena_for(Batch& b, uint64_t bytes) {
+  // b gets an arena of at least `bytes`: a spare one when one is big enough;
+  // false if it cannot be allocated (caller holds mu_)
+  bool arena_for(Batch& b, uint64_t bytes) {
     for (auto it = spare_.begin(); it != spare_.end(); ++it)
       if (it->second >= bytes) {
         b.arena = std::move(it->first);
         b.cap = it->second;
         spare_.erase(it);
-        return;
+        return true;
       }
-    b.arena.reset(new uint8_t[bytes]);  // not value-initialised: untouched pages cost nothing
-    b.cap = bytes;
+    // not value-initialised: untouched pages cost nothing
+    b.arena.reset(new (std::nothrow) uint8_t[bytes]);
+    b.cap = b.arena ? bytes : 0;
+    return b.arena != nullptr;
   }
 
   void evict() {  // caller holds mu_

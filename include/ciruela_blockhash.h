@@ -50,6 +50,9 @@ extern "C" {
 #define CIR_DIGEST_BYTES 32
 #define CIR_DEFAULT_BLOCK_SIZE 32768 /* src/daemon/disk/public.rs:154 */
 
+/* Every int-returning call returns one of these (the text of the last
+ * failure on this thread: cir_last_error).  No C++ exception leaves the
+ * library: an allocation that fails inside it is CIR_ENOMEM. */
 enum cir_status {
   CIR_OK = 0,
   CIR_EIO = -1,        /* filesystem error: scan's io::Error (src/client/sync/uploads.rs:57) */
@@ -301,7 +304,7 @@ int cir_index_rewrite(cir_ctx* ctx, const uint8_t* in, size_t len, uint8_t** out
 
 /* InMemoryIndexes (src/index.rs:53-124): ImageId -> index bytes. */
 typedef struct cir_indexes cir_indexes;
-cir_indexes* cir_indexes_new(void);
+cir_indexes* cir_indexes_new(void); /* NULL if out of memory */
 void cir_indexes_free(cir_indexes* h);
 /* register_index (src/index.rs:98-105); id_out holds 64 bytes. */
 int cir_indexes_register(cir_indexes* h, const uint8_t* data, size_t len, uint8_t* id_out,
@@ -312,7 +315,7 @@ int cir_indexes_read(cir_indexes* h, const uint8_t* id, size_t id_len, uint8_t**
 
 /* ThreadedBlockReader (src/blocks.rs:85-240): BlockHash -> block bytes. */
 typedef struct cir_blocks cir_blocks;
-cir_blocks* cir_blocks_new(void);
+cir_blocks* cir_blocks_new(void); /* NULL if out of memory */
 void cir_blocks_free(cir_blocks* h);
 size_t cir_blocks_len(cir_blocks* h);
 /* register_dir (src/blocks.rs:145-183): CIR_EPARSE / CIR_EHASHSIZE. */

@@ -330,3 +330,46 @@ def test_product_never_loads_the_oracle():
         for bad in ("liboracle", "blake2b_oracle", "import cpu_indexer", "import dirsig_oracle",
                     "oracle/"):
             assert bad not in text, (p, bad)
+
+
+def test_cli_rejects_bad_numbers(tmp_path):
+    """--disk-threads / --block-size take a decimal count; anything else is a
+    usage error (exit 2), not an uncaught exception out of main."""
+    cli = os.path.join(ROOT, "bin", "ciruela-index")
+    for flag, v in [("--disk-threads", "abc"), ("--block-size", "-5"), ("--block-size", "12x"),
+                    ("--disk-threads", "99999999999"), ("--block-size", "")]:
+        p = subprocess.run([cli, "sync", flag, v, "--append", "%s:/d" % tmp_path],
+                           capture_output=True)
+        assert p.returncode == 2, (flag, v, p.stderr)
+        assert b"invalid value for " + flag.encode() in p.stderr
+
+
+_ENOMEM_CHILD = r"""
+import ctypes, resource, sys
+sys.path.insert(0, sys.argv[1])
+from ciruela_amd import _native
+lib = _native.lib
+lines = ["DIRSIGNATURE.v1 blake2b/256 block_size=32768", "/"]
+lines += ["  f%07d f 100 %s" % (i, "ab" * 32) for i in range(1000000)]
+index = ("\n".join(lines) + "\n" + "00" * 32 + "\n").encode()
+h = lib.cir_indexes_new()
+assert h
+vm = [int(l.split()[1]) for l in open("/proc/self/status") if l.startswith("VmSize:")][0] * 1024
+resource.setrlimit(resource.RLIMIT_AS, (vm + (32 << 20), resource.RLIM_INFINITY))
+out = ctypes.create_string_buffer(64)
+n = ctypes.c_size_t()
+rc = lib.cir_indexes_register(h, index, len(index), out, ctypes.byref(n))
+print(rc, lib.cir_last_error().decode())
+"""
+
+
+def test_no_exception_crosses_the_abi():
+    """A host allocation that fails inside the library comes back as
+    CIR_ENOMEM with its text in cir_last_error -- not std::terminate (and
+    never an unwind into a Rust caller).  A child process parses a 1M-file
+    index with 32 MiB of address space to spare."""
+    p = subprocess.run(["python3", "-c", _ENOMEM_CHILD, ROOT], capture_output=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    rc, _, msg = p.stdout.decode().strip().partition(" ")
+    assert int(rc) == _native.CIR_ENOMEM, p.stdout
+    assert "C++ exception" in msg

@@ -2207,6 +2207,25 @@ def test_verify_async_forget_and_expiry(gpu, oracle):
     c.close()
 
 
+def test_verify_arena_that_cannot_be_allocated(gpu, oracle):
+    """A queue bound so large that a new batch's arena (half of it) cannot
+    be allocated: the submit fails with CIR_ENOMEM and holds nothing (no
+    exception out of the library), and the queue works again at the default
+    bound."""
+    from ciruela_amd import _native as n
+    c = gpu.Context(device_mask=1, staging_bytes=1 << 20)
+    blk = os.urandom(32768)
+    want = oracle_digest(oracle, blk)
+    c.verify_limits(max_bytes=1 << 62)
+    with pytest.raises(n.CiruelaError) as e:
+        c.verify_submit(blk, want)
+    assert e.value.status == n.CIR_ENOMEM, e.value
+    assert c.verify_stats()["bytes_held"] == 0
+    c.verify_limits()
+    assert c.verify_wait(c.verify_submit(blk, want)) is True
+    c.close()
+
+
 def host_case(gpu, oracle, seed, tmp_path, monkeypatch):
     """One randomized round of the host-memory entry points against the
     oracle, over the staging knobs: staging size, copy mode, 1-3 device
