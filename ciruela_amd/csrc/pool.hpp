@@ -7,8 +7,10 @@
 #include <algorithm>
 #include <condition_variable>
 #include <deque>
+#include <exception>
 #include <functional>
 #include <mutex>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -19,6 +21,10 @@ namespace cir {
 // from shared state and returns when none are left, so once the caller's own
 // run returns, tickets nobody has started are dropped rather than waited
 // for: a busy pool delays a call by at most the tickets already running.
+// Exceptions: a job that throws (in the caller or in a worker) is still
+// waited for everywhere it runs, and run() rethrows the first exception once
+// no copy is left running; a worker thread that cannot be created leaves its
+// ticket to the running workers or to the caller's own run.
 class WorkerPool {
  public:
   static constexpr size_t kMaxWorkers = 256;
@@ -51,10 +57,20 @@ class WorkerPool {
       // a worker for every ticket queued or running, concurrent callers
       // included (several devices' readers at once)
       const size_t want = std::min<size_t>(busy_ + q_.size(), kMaxWorkers);
-      while (th_.size() < want) th_.emplace_back([this] { loop(); });
+      try {
+        while (th_.size() < want) th_.emplace_back([this] { loop(); });
+      } catch (const std::system_error&) {
+        // (no thread for now: the tickets wait for a free worker or are
+        // dropped once the caller's own run has done the work)
+      }
     }
     cv_.notify_all();
-    fn();
+    std::exception_ptr mine;
+    try {
+      fn();
+    } catch (...) {
+      mine = std::current_exception();
+    }
     std::unique_lock<std::mutex> lk(mu_);
     for (auto it = q_.begin(); it != q_.end();) {
       if (*it == &job) {
@@ -65,6 +81,9 @@ class WorkerPool {
       }
     }
     job.done.wait(lk, [&] { return job.pending == 0; });
+    if (!mine) mine = job.error;
+    lk.unlock();
+    if (mine) std::rethrow_exception(mine);
   }
 
   size_t workers() {
@@ -77,6 +96,7 @@ class WorkerPool {
     const std::function<void()>* fn = nullptr;
     unsigned pending = 0;  // tickets queued or running (under mu_)
     std::condition_variable done;
+    std::exception_ptr error;  // the first a worker's copy threw (under mu_)
   };
 
   void loop() {
@@ -88,8 +108,14 @@ class WorkerPool {
       q_.pop_front();
       ++busy_;
       lk.unlock();
-      (*j->fn)();
+      std::exception_ptr e;
+      try {
+        (*j->fn)();
+      } catch (...) {
+        e = std::current_exception();
+      }
       lk.lock();
+      if (e && !j->error) j->error = e;
       --busy_;
       if (--j->pending == 0) j->done.notify_all();
     }

@@ -20,6 +20,7 @@
 #include <condition_variable>
 #include <cstdlib>
 #include <deque>
+#include <exception>
 #include <new>
 #include <system_error>
 #include <thread>
@@ -172,6 +173,32 @@ static WorkerPool& pool() {  // never destroyed: a context's threads may still u
 }
 
 void parallel_run(unsigned n, const std::function<void()>& work) { pool().run(n, work); }
+
+void fan_out(size_t n, const std::function<void(size_t)>& fn) {
+  std::vector<std::exception_ptr> errs(n);
+  auto one = [&](size_t i) {
+    try {
+      fn(i);
+    } catch (...) {
+      errs[i] = std::current_exception();
+    }
+  };
+  std::vector<std::thread> th;
+  std::vector<size_t> here;
+  th.reserve(n);
+  here.reserve(n);
+  for (size_t i = 0; i < n; ++i) {
+    try {
+      th.emplace_back(one, i);
+    } catch (const std::system_error&) {
+      here.push_back(i);  // no thread: run it on this one below
+    }
+  }
+  for (size_t i : here) one(i);
+  for (auto& t : th) t.join();
+  for (auto& e : errs)
+    if (e) std::rethrow_exception(e);
+}
 
 bool scan_ramp() {  // read per call
   const char* v = std::getenv("CIR_STAGE_RAMP");
@@ -571,13 +598,10 @@ static int for_each_device(cir_ctx* ctx, const std::function<int(cir::Device&, s
   if (nd == 1) return fn(*ctx->devs[0], 0);
   std::vector<int> rc(nd, 0);
   std::vector<std::string> err(nd);
-  std::vector<std::thread> th;
-  for (size_t i = 0; i < nd; ++i)
-    th.emplace_back([&, i] {
-      rc[i] = fn(*ctx->devs[i], i);
-      if (rc[i]) err[i] = t_last_error;
-    });
-  for (auto& t : th) t.join();
+  fan_out(nd, [&](size_t i) {
+    rc[i] = fn(*ctx->devs[i], i);
+    if (rc[i]) err[i] = t_last_error;
+  });
   for (size_t i = 0; i < nd; ++i)
     if (rc[i]) return fail(rc[i], err[i]);
   return CIR_OK;
@@ -717,29 +741,26 @@ static int run_split(cir_ctx* ctx, const PosReader& prd, uint64_t total, uint64_
   }
   std::vector<int> rc(nd, 0);
   std::vector<std::string> err(nd);
-  std::vector<std::thread> th;
-  for (size_t i = 0; i < nd; ++i)
-    th.emplace_back([&, i] {
-      const uint64_t beg = lo[i] * bs, end = std::min(hi[i] * bs, total);
-      uint64_t pos = beg;
-      Reader rd = [&](uint8_t* dst, uint64_t n) -> int64_t {
-        const uint64_t k = std::min(n, end - pos);
-        if (k == 0) return 0;
-        const int64_t r = prd(dst, k, pos);
-        if (r < 0) return r;
-        pos += k;
-        return (int64_t)k;
-      };
-      HashBuf h;
-      uint64_t got = 0;
-      rc[i] = run_file_dev(ctx, *ctx->devs[i], rd, bs, &got, h, ht, end - beg, /*exact=*/true);
-      if (!rc[i] && h.len != 32 * (hi[i] - lo[i])) rc[i] = fail(CIR_EIO, "short range");
-      if (rc[i])
-        err[i] = t_last_error;
-      else
-        memcpy(hashes.p + 32 * lo[i], h.p, h.len);
-    });
-  for (auto& t : th) t.join();
+  fan_out(nd, [&](size_t i) {
+    const uint64_t beg = lo[i] * bs, end = std::min(hi[i] * bs, total);
+    uint64_t pos = beg;
+    Reader rd = [&](uint8_t* dst, uint64_t n) -> int64_t {
+      const uint64_t k = std::min(n, end - pos);
+      if (k == 0) return 0;
+      const int64_t r = prd(dst, k, pos);
+      if (r < 0) return r;
+      pos += k;
+      return (int64_t)k;
+    };
+    HashBuf h;
+    uint64_t got = 0;
+    rc[i] = run_file_dev(ctx, *ctx->devs[i], rd, bs, &got, h, ht, end - beg, /*exact=*/true);
+    if (!rc[i] && h.len != 32 * (hi[i] - lo[i])) rc[i] = fail(CIR_EIO, "short range");
+    if (rc[i])
+      err[i] = t_last_error;
+    else
+      memcpy(hashes.p + 32 * lo[i], h.p, h.len);
+  });
   for (size_t i = 0; i < nd; ++i)
     if (rc[i]) return fail(rc[i], err[i]);
   return CIR_OK;
@@ -847,13 +868,10 @@ static int init_devices(std::vector<std::unique_ptr<Device>>& devs, uint64_t sta
   }
   std::vector<int> rc(devs.size(), 0);
   std::vector<std::string> err(devs.size());
-  std::vector<std::thread> th;
-  for (size_t i = 0; i < devs.size(); ++i)
-    th.emplace_back([&, i] {
-      rc[i] = init_device(*devs[i], staging, lazy, one_shot);
-      if (rc[i]) err[i] = t_last_error;
-    });
-  for (auto& t : th) t.join();
+  fan_out(devs.size(), [&](size_t i) {
+    rc[i] = init_device(*devs[i], staging, lazy, one_shot);
+    if (rc[i]) err[i] = t_last_error;
+  });
   for (size_t i = 0; i < devs.size(); ++i)
     if (rc[i]) return fail(rc[i], err[i]);
   return CIR_OK;

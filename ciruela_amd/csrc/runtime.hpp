@@ -116,6 +116,12 @@ bool stage_copy_nt();
 // left: copies still queued when the caller's own copy returns are dropped.
 // Round 4: the host paths created their reader / copy threads per batch.
 void parallel_run(unsigned n, const std::function<void()>& work);
+// Run fn(i) for every i in [0, n), each on a thread of its own (one per
+// device state), and return once all have returned.  A thread that cannot
+// be created runs its i on the calling thread instead; an exception thrown
+// by any fn(i) is rethrown after every thread has been joined (the entry
+// point's CIR_CATCH_BOUNDARY turns it into a code).
+void fan_out(size_t n, const std::function<void(size_t)>& fn);
 // CIR_STAGE_RAMP=0: the staged host paths (scan, hash_file, hash_memory)
 // start with whole-slot batches instead of ramping up from 1/8 of a slot.
 bool scan_ramp();

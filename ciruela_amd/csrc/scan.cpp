@@ -426,14 +426,11 @@ static int hash_files(cir_ctx* ctx, std::vector<ScanFile>& files, uint64_t bs, u
   const unsigned per = std::max(1u, threads / (unsigned)nd);
   std::vector<int> rc(nd, 0);
   std::vector<std::string> err(nd);
-  std::vector<std::thread> th;
-  for (size_t i = 0; i < nd; ++i)
-    th.emplace_back([&, i] {
-      rc[i] = hash_range(ctx, *ctx->devs[i], i, files, bs, per, ht, digests, dev_ranges[i],
-                         [&, i](size_t r, uint64_t n) { return done(i, r, n); }, scan_t0);
-      if (rc[i]) err[i] = cir_last_error();
-    });
-  for (auto& t : th) t.join();
+  fan_out(nd, [&](size_t i) {
+    rc[i] = hash_range(ctx, *ctx->devs[i], i, files, bs, per, ht, digests, dev_ranges[i],
+                       [&, i](size_t r, uint64_t n) { return done(i, r, n); }, scan_t0);
+    if (rc[i]) err[i] = cir_last_error();
+  });
   for (size_t i = 0; i < nd; ++i)
     if (rc[i]) return fail(rc[i], err[i]);
   CIR_HIP(hipSetDevice(dev0));

@@ -285,11 +285,12 @@ class VerifyQueue {
       writers_cv_.wait(lk, [&] { return bp->writers == 0; });  // every block copied in
       lk.unlock();
       const size_t n = bp->tickets.size();
-      std::vector<uint8_t> got(32 * n);
       static const uint8_t empty = 0;
       std::string err;
-      const int rc = hash_(bp->ht, bp->used ? bp->arena.get() : &empty, bp->off.data(),
-                           bp->len.data(), n, got.data(), &err);
+      std::unique_ptr<uint8_t[]> got(new (std::nothrow) uint8_t[32 * n]);
+      const int rc = got ? hash_(bp->ht, bp->used ? bp->arena.get() : &empty, bp->off.data(),
+                                 bp->len.data(), n, got.get(), &err)
+                         : (err = "verify batch digests", CIR_ENOMEM);
       const uint64_t bytes = bp->used;
       lk.lock();
       for (size_t i = 0; i < n; ++i) {
@@ -299,7 +300,7 @@ class VerifyQueue {
           done_[t] = rc;
           errors_[t] = err;
         } else {
-          done_[t] = memcmp(got.data() + 32 * i, bp->expected.data() + 32 * i, 32) == 0 ? 1 : 2;
+          done_[t] = memcmp(got.get() + 32 * i, bp->expected.data() + 32 * i, 32) == 0 ? 1 : 2;
         }
       }
       held_ -= bytes;
