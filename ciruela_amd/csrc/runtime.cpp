@@ -652,18 +652,25 @@ static int run_file_dev(cir_ctx* ctx, Device& d, const Reader& rd, uint64_t bs,
   DeviceGuard guard;
   CIR_HIP(hipSetDevice(d.id));
   SlotDrain drain{d};  // an early return leaves no slot busy
-  uint64_t chunk = ctx->staging / bs * bs;
-  if (chunk == 0) chunk = bs;
-  // an exact source shorter than one block is one short block: a slot of
-  // its own size, not of the block size (a huge block size over a small
-  // input would otherwise pin and allocate a block-sized slot)
-  const bool one_short = exact && size_hint < bs;
-  if (one_short) chunk = std::max<uint64_t>(16, (size_hint + 15) & ~15ull);
-  const uint64_t chunk_blk = one_short ? 1 : chunk / bs;
+  const uint64_t block_chunk = std::max<uint64_t>(bs, ctx->staging / bs * bs);
+  uint64_t chunk = block_chunk;
+  // A source shorter than one block is one short block: a slot of its own
+  // size, not of the block size (a huge block size over a small input would
+  // otherwise pin and allocate a block-sized slot).  A file whose size is
+  // only a lower bound (it may grow while it is read) gets one byte of room
+  // more: a slot that fills up means it grew, and the slot is regrown to
+  // the block form with the bytes read so far.
+  const bool one_short = (exact || size_hint > 0) && size_hint < bs;
+  bool may_grow = one_short && !exact;
+  if (one_short)
+    chunk = std::max<uint64_t>(16, (std::min(bs, size_hint + (may_grow ? 1 : 0)) + 15) & ~15ull);
+  uint64_t chunk_blk = one_short ? 1 : chunk / bs;
   // the first batches ramp up (1/8, 1/4, 1/2 of a slot, then whole slots),
   // as the scan's do: the first upload starts after a short fill
-  uint64_t fill = one_short ? chunk
-                            : scan_ramp() ? std::max<uint64_t>(bs, chunk / 8 / bs * bs) : chunk;
+  auto first_fill = [&] {
+    return scan_ramp() ? std::max<uint64_t>(bs, block_chunk / 8 / bs * bs) : block_chunk;
+  };
+  uint64_t fill = one_short ? chunk : first_fill();
   uint64_t total = 0;
   bool eof = false;
   size_t pending_at[2] = {0, 0}, pending_n[2] = {0, 0};
@@ -682,16 +689,32 @@ static int run_file_dev(cir_ctx* ctx, Device& d, const Reader& rd, uint64_t bs,
       int rc = d.ensure_slot(s, chunk, chunk_blk);
       if (rc) return rc;
       uint64_t got = 0;
-      const uint64_t want = fill;
+      uint64_t want = fill;
       fill = std::min(chunk, fill * 2);
-      while (got < want) {
-        const int64_t r = rd(s.h_data + got, want - got);
-        if (r < 0) return fail(CIR_EIO, std::string("read: ") + strerror((int)-r));
-        if (r == 0) {
-          eof = true;
-          break;
+      for (;;) {
+        while (got < want) {
+          const int64_t r = rd(s.h_data + got, want - got);
+          if (r < 0) return fail(CIR_EIO, std::string("read: ") + strerror((int)-r));
+          if (r == 0) {
+            eof = true;
+            break;
+          }
+          got += (uint64_t)r;
         }
-        got += (uint64_t)r;
+        if (!may_grow || eof || got < want) break;
+        // the file grew past its size at the start: the block form from here
+        // (this slot regrown around the bytes already read)
+        may_grow = false;
+        std::unique_ptr<uint8_t[]> head(new (std::nothrow) uint8_t[got]);
+        if (!head) return fail(CIR_ENOMEM, "read buffer");
+        memcpy(head.get(), s.h_data, got);
+        chunk = block_chunk;
+        chunk_blk = chunk / bs;
+        rc = d.ensure_slot(s, chunk, chunk_blk);
+        if (rc) return rc;
+        memcpy(s.h_data, head.get(), got);
+        want = std::max(got, first_fill());
+        fill = std::min(chunk, want * 2);
       }
       if (got > 0) {
         const uint64_t n = (got + bs - 1) / bs;
@@ -1305,6 +1328,10 @@ int cir_hash_file_ht(cir_ctx* ctx, int hash_type, int fd, uint64_t block_size,
   uint64_t known = 0, done = 0;
   if (pos0 >= 0 && ::fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && st.st_size > pos0)
     known = (uint64_t)(st.st_size - pos0);
+  // CIR_DEBUG_GROW=k (tests): take the file to be k bytes shorter than
+  // fstat says, as if it grew by k between the fstat and the reads
+  if (const char* v = std::getenv("CIR_DEBUG_GROW"))
+    known -= std::min<uint64_t>(known, strtoull(v, nullptr, 10));
   if (known > 0 && ctx->devs.size() > 1 && known > block_size) {
     // several devices: split the known bytes, then make sure nothing follows
     // (a file growing meanwhile is re-hashed on one device, to its end)

@@ -1870,7 +1870,8 @@ def test_extreme_block_sizes(gpu, oracle, tmp_path):
     byte or seven), and 2^32-1 over small inputs -- one short block per file,
     in slots sized to the input, not the block size (the process's resident
     memory grows by far less than one such block).  Scan, hash_memory,
-    hash_file; every digest and the index equal the oracles'."""
+    hash_file (a regular file shorter than a block: a slot of its size plus
+    one byte); every digest and the index equal the oracles'."""
     c = gpu.Context(device_mask=1, staging_bytes=1 << 20)
     rng = random.Random(93)
 
@@ -1888,17 +1889,39 @@ def test_extreme_block_sizes(gpu, oracle, tmp_path):
         data = rng.randbytes(3000)
         want = b"".join(oracle_digest(oracle, data[i:i + bs]) for i in range(0, len(data), bs))
         assert c.hash_memory(data, bs) == want, bs
-        assert rss() - rss0 < (512 << 20), (bs, (rss() - rss0) >> 20)
-        if bs > (1 << 30):
-            # a regular file may grow while hash_file reads it to EOF, so that
-            # path keeps one block-sized slot (4 GiB pinned here): not run
-            continue
         p = root / "d" / "f5"
         with open(p, "rb") as f:
             size, hashes = c.hash_file(f.fileno(), bs)
         blob = p.read_bytes()
         assert size == 5000 and hashes == b"".join(
             oracle_digest(oracle, blob[i:i + bs]) for i in range(0, len(blob), bs)), bs
+        assert rss() - rss0 < (512 << 20), (bs, (rss() - rss0) >> 20)
+    c.close()
+
+
+@pytest.mark.parametrize("size,hint_short", [(1000, 600), (1000, 999), (3 << 20, (3 << 20) - 100),
+                                             (5000, 4984), (17, 1)])
+def test_hash_file_that_grows(gpu, oracle, tmp_path, monkeypatch, size, hint_short):
+    """cir_hash_file on a regular file that grows between its fstat and its
+    reads (CIR_DEBUG_GROW: the file taken to be hint_short bytes shorter):
+    a size below one block gets a slot of that size plus one byte, finds it
+    full, and regrows it to the block form around the bytes already read --
+    the digests are the whole file's, as Hashes::hash_file's read-to-EOF
+    loop gives."""
+    bs = (1 << 20) + 5
+    c = gpu.Context(device_mask=1, staging_bytes=1 << 20)
+    blob = os.urandom(size)
+    p = tmp_path / "grows.bin"
+    p.write_bytes(blob)
+    monkeypatch.setenv("CIR_DEBUG_GROW", str(hint_short))
+    for skip in (0, 3):
+        with open(p, "rb") as f:
+            f.seek(skip)
+            got, hashes = c.hash_file(f.fileno(), bs)
+        tail = blob[skip:]
+        assert got == len(tail)
+        assert hashes == b"".join(oracle_digest(oracle, tail[i:i + bs])
+                                  for i in range(0, len(tail), bs)), (size, hint_short, skip)
     c.close()
 
 
@@ -2268,9 +2291,6 @@ def host_case(gpu, oracle, seed, tmp_path, monkeypatch):
     blob = arena[:size]
     chunks = b"".join(h(blob[i:i + bs]) for i in range(0, size, bs))
     assert c.hash_memory(blob, bs, ht) == chunks, seed
-    if bs > (1 << 30):  # hash_file keeps a block-sized slot (4 GiB pinned): not drawn
-        c.close()
-        return
     p = tmp_path / ("f%d.bin" % seed)
     p.write_bytes(blob)
     skip = rng.randrange(0, size + 1)
