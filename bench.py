@@ -946,7 +946,7 @@ def make_config1_tree(root):
 CONFIG1_ROOT = "/tmp/ciruela_cfg1_tree"
 
 
-def time_cli_config1(runs=6):
+def time_cli_config1(runs=10):
     """`ciruela-index sync --append` of the config-1 tree as separate
     processes, timed from the parent's side (fork + exec + HIP start-up +
     scan + exit).  bench.py calls it before it touches a GPU itself (no
