@@ -9,7 +9,8 @@ ASan + UBSan (tools/verify_queue_stress.cpp):
     bound is taken alone; forget of a pending ticket (releasing its waiter),
     of a finished one and of an unknown one; expiry keeps the newest
     max_results outcomes; a failed batch reports its code to every ticket;
-    two hash types never share a batch;
+    two hash types never share a batch; an arena that cannot be allocated
+    is CIR_ENOMEM;
   * random traffic from 2-5 threads, blocking and not, with forgets and
     polls: every outcome right, the peak within the bound, nothing held at
     the end, and a queue destroyed with work queued drains it.
@@ -35,6 +36,10 @@ def test_verify_queue_sanitized(tmp_path, san):
                     "-I" + os.path.join(ROOT, "include"),
                     os.path.join(ROOT, "tools", "verify_queue_stress.cpp"), "-o", exe,
                     "-lpthread"], check=True)
-    p = subprocess.run([exe, "6", "7"], capture_output=True, timeout=300)
+    # (a queue bound past what can be allocated must come back as CIR_ENOMEM:
+    # the sanitizers' allocators return null for it instead of aborting)
+    env = dict(os.environ, ASAN_OPTIONS="allocator_may_return_null=1",
+               TSAN_OPTIONS="allocator_may_return_null=1")
+    p = subprocess.run([exe, "6", "7"], capture_output=True, timeout=300, env=env)
     assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
     assert p.stdout.startswith(b"ok ") and b"WARNING: ThreadSanitizer" not in p.stderr

@@ -259,6 +259,17 @@ static void deterministic(std::mt19937_64& rng) {
   uint64_t tz = 0;
   CHECK(q.submit(1, big.data.data(), big.data.size(), big.expected, &tz, &err) == 0);
   CHECK(q.wait(tz, &err) == 1);
+  // a bound past what can be allocated: a new batch's arena (half of it)
+  // fails, the submit is CIR_ENOMEM and holds nothing; the queue works
+  // again at the default bound
+  stage("arena that cannot be allocated");
+  q.limits(1ull << 62, 0, false);
+  uint64_t tn = 0;
+  CHECK(q.submit(1, p2.data.data(), 10, p2.expected, &tn, &err) == CIR_ENOMEM);
+  CHECK(stat(q, kHeld) == 0);
+  q.limits(0, 0, false);
+  CHECK(q.submit(1, p2.data.data(), 10, p2.expected, &tn, &err) == 0);
+  CHECK(q.wait(tn, &err) == 1);
 }
 
 // random traffic from several threads against a byte bound, blocking or
