@@ -22,7 +22,7 @@ OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS_HIP)) \
         $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(SRCS_CPP))
 HDRS := $(wildcard $(CSRC)/*.hpp) include/ciruela_blockhash.h
 
-all: $(LIB) $(CLI) build/hash_bytes_conc build/verify_daemon_sim oracle
+all: $(LIB) $(CLI) build/hash_bytes_conc build/verify_daemon_sim build/host_asan_driver oracle
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -53,6 +53,22 @@ build/verify_daemon_sim: tools/verify_daemon_sim.cpp $(LIB) include/ciruela_bloc
 	$(HIPCC) $(HOSTFLAGS) $< -o $@ -Lciruela_amd -lciruela_amd \
 	    -Wl,-rpath,'$$ORIGIN/../ciruela_amd' -lpthread
 
+# the library's host code under ASan + UBSan against the production device
+# code (tools/host_asan_driver.cpp; sanitizers on the host side only)
+ASAN_HOST := -O1 -g -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
+             -Xarch_host -fno-sanitize-recover=all -Xarch_host -fno-omit-frame-pointer
+ASAN_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS_HIP)) \
+             $(patsubst $(CSRC)/%.cpp,build/asan/%.o,$(SRCS_CPP)) build/asan/host_asan_driver.o
+build/asan/%.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p build/asan
+	$(HIPCC) $(HOSTFLAGS) $(ASAN_HOST) -c $< -o $@
+build/asan/host_asan_driver.o: tools/host_asan_driver.cpp include/ciruela_blockhash.h
+	@mkdir -p build/asan
+	$(HIPCC) $(HOSTFLAGS) $(ASAN_HOST) -c $< -o $@
+build/host_asan_driver: $(ASAN_OBJS)
+	$(HIPCC) $(HIPFLAGS) $(ASAN_HOST) -o $@ $(ASAN_OBJS) -lpthread
+asan: build/host_asan_driver
+
 oracle:
 	$(MAKE) -C oracle
 
@@ -60,4 +76,4 @@ clean:
 	rm -rf build $(LIB) $(CLI)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean asan

@@ -644,10 +644,12 @@ struct HashBuf {
 };
 
 // size_hint: the source's length when known (a lower bound for a file that
-// may grow); `exact`: the source ends there (memory, a known range).
+// may grow), kSizeUnknown otherwise (a pipe); `exact`: the source ends there
+// (memory, a known range).
+constexpr uint64_t kSizeUnknown = ~0ull;
 static int run_file_dev(cir_ctx* ctx, Device& d, const Reader& rd, uint64_t bs,
-                        uint64_t* size_out, HashBuf& hashes, int ht, uint64_t size_hint = 0,
-                        bool exact = false) {
+                        uint64_t* size_out, HashBuf& hashes, int ht,
+                        uint64_t size_hint = kSizeUnknown, bool exact = false) {
   std::lock_guard<std::mutex> lk(d.mu);
   DeviceGuard guard;
   CIR_HIP(hipSetDevice(d.id));
@@ -660,7 +662,9 @@ static int run_file_dev(cir_ctx* ctx, Device& d, const Reader& rd, uint64_t bs,
   // only a lower bound (it may grow while it is read) gets one byte of room
   // more: a slot that fills up means it grew, and the slot is regrown to
   // the block form with the bytes read so far.
-  const bool one_short = (exact || size_hint > 0) && size_hint < bs;
+  const bool hinted = size_hint != kSizeUnknown;
+  if (!hinted) size_hint = 0;
+  const bool one_short = (exact || hinted) && size_hint < bs;
   bool may_grow = one_short && !exact;
   if (one_short)
     chunk = std::max<uint64_t>(16, (std::min(bs, size_hint + (may_grow ? 1 : 0)) + 15) & ~15ull);
@@ -670,7 +674,9 @@ static int run_file_dev(cir_ctx* ctx, Device& d, const Reader& rd, uint64_t bs,
   auto first_fill = [&] {
     return scan_ramp() ? std::max<uint64_t>(bs, block_chunk / 8 / bs * bs) : block_chunk;
   };
-  uint64_t fill = one_short ? chunk : first_fill();
+  // (a file that may grow reads one byte past its size, never more than one
+  // block: more bytes than that and it regrows below)
+  uint64_t fill = !one_short ? first_fill() : may_grow ? size_hint + 1 : chunk;
   uint64_t total = 0;
   bool eof = false;
   size_t pending_at[2] = {0, 0}, pending_n[2] = {0, 0};
@@ -741,7 +747,8 @@ static int run_file_dev(cir_ctx* ctx, Device& d, const Reader& rd, uint64_t bs,
 }
 
 static int run_file(cir_ctx* ctx, const Reader& rd, uint64_t bs, uint64_t* size_out,
-                    HashBuf& hashes, int ht, uint64_t size_hint = 0, bool exact = false) {
+                    HashBuf& hashes, int ht, uint64_t size_hint = kSizeUnknown,
+                    bool exact = false) {
   return run_file_dev(ctx, *ctx->devs[0], rd, bs, size_out, hashes, ht, size_hint, exact);
 }
 
@@ -1326,8 +1333,8 @@ int cir_hash_file_ht(cir_ctx* ctx, int hash_type, int fd, uint64_t block_size,
   struct stat st;
   const off_t pos0 = ::lseek(fd, 0, SEEK_CUR);
   uint64_t known = 0, done = 0;
-  if (pos0 >= 0 && ::fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && st.st_size > pos0)
-    known = (uint64_t)(st.st_size - pos0);
+  const bool regular = pos0 >= 0 && ::fstat(fd, &st) == 0 && S_ISREG(st.st_mode);
+  if (regular && st.st_size > pos0) known = (uint64_t)(st.st_size - pos0);
   // CIR_DEBUG_GROW=k (tests): take the file to be k bytes shorter than
   // fstat says, as if it grew by k between the fstat and the reads
   if (const char* v = std::getenv("CIR_DEBUG_GROW"))
@@ -1395,7 +1402,9 @@ int cir_hash_file_ht(cir_ctx* ctx, int hash_type, int fd, uint64_t block_size,
       return r < 0 ? -(int64_t)errno : (int64_t)r;
     }
   };
-  int rc = run_file(ctx, rd, block_size, size_out, h, hash_type, known);
+  // (a regular file's size at the fstat is a lower bound: an empty one
+  // gets a 16-byte slot, not a block-sized one)
+  int rc = run_file(ctx, rd, block_size, size_out, h, hash_type, regular ? known : kSizeUnknown);
   if (rc) return rc;
   return export_hashes(h, hashes_out, nhash_out);
 } CIR_CATCH_BOUNDARY

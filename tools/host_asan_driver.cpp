@@ -1,0 +1,287 @@
+// The library's host code under AddressSanitizer + UBSan, on a real GPU.
+// The device code is the production build; every host translation unit
+// (runtime, scan, dirsig, registry, the host hashers) is instrumented
+// (make build/host_asan_driver: -fsanitize after -Xarch_host, host only).
+// Each round drives the host-path entry points over random inputs through
+// one of three contexts -- plain (1 MiB staging), three device states on the
+// one GPU (CIR_DEBUG_SPLIT=3) and one-shot -- and checks every GPU digest
+// against the library's host hashers (cir_debug_host_*, themselves checked
+// against the oracle in the CPU suite): descriptor batches in both hash
+// types, batch verify with wrong digests, hash_memory and hash_file at block
+// sizes up to 2^32-1 (a file that grows, CIR_DEBUG_GROW), the asynchronous
+// verify with forgets, scans returned whole and written out as they go,
+// the rewrite, and the registries.  Any memory error or undefined behaviour
+// ends the run with the sanitizer's report.
+//   build/host_asan_driver [rounds=40] [seed=1]
+//   (ASAN_OPTIONS=detect_leaks=0: the HIP runtime keeps its allocations)
+#include <fcntl.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <random>
+#include <string>
+#include <vector>
+
+#include "ciruela_blockhash.h"
+
+static int g_fail = 0;
+#define CHECK(c)                                                                     \
+  do {                                                                               \
+    if (!(c)) {                                                                      \
+      fprintf(stderr, "FAIL %s:%d: %s (%s)\n", __FILE__, __LINE__, #c, cir_last_error()); \
+      ++g_fail;                                                                      \
+      return;                                                                        \
+    }                                                                                \
+  } while (0)
+
+static std::mt19937_64 rng;
+static uint64_t pick(std::initializer_list<uint64_t> v) {
+  return v.begin()[rng() % v.size()];
+}
+static std::vector<uint8_t> random_bytes(size_t n) {
+  std::vector<uint8_t> b(n);
+  for (size_t i = 0; i < n; i += 8) {
+    const uint64_t x = rng();
+    memcpy(b.data() + i, &x, std::min<size_t>(8, n - i));
+  }
+  return b;
+}
+static void host_digest(int ht, const uint8_t* p, size_t n, uint8_t out[32]) {
+  if (ht == CIR_HASH_SHA512_256)
+    cir_debug_host_sha512_256(p, n, 4096, out);
+  else
+    cir_debug_host_blake2b256(p, n, 4096, out);
+}
+static std::vector<uint8_t> chunk_digests(int ht, const uint8_t* p, size_t n, uint64_t bs) {
+  std::vector<uint8_t> d;
+  for (uint64_t o = 0; o < n; o += bs) {
+    uint8_t h[32];
+    host_digest(ht, p + o, (size_t)std::min<uint64_t>(bs, n - o), h);
+    d.insert(d.end(), h, h + 32);
+  }
+  return d;
+}
+
+static void descriptors(cir_ctx* ctx, int ht) {
+  std::vector<uint8_t> arena = random_bytes(pick({1 << 16, 3 << 20}));
+  const size_t n = pick({1, 7, 300, 1500});
+  std::vector<uint64_t> off(n);
+  std::vector<uint32_t> len(n);
+  for (size_t i = 0; i < n; ++i) {
+    len[i] = (uint32_t)std::min<uint64_t>(pick({0, 1, 127, 128, 129, 4096, 32768, rng() % 70000}),
+                                          arena.size());
+    off[i] = rng() % (arena.size() - len[i] + 1);
+  }
+  std::vector<uint8_t> got(32 * n), want(32 * n);
+  CHECK(cir_hash_blocks_ht(ctx, ht, arena.data(), off.data(), len.data(), n, got.data()) == 0);
+  for (size_t i = 0; i < n; ++i) host_digest(ht, arena.data() + off[i], len[i], &want[32 * i]);
+  CHECK(got == want);
+  std::vector<uint8_t> exp = want, ok(n);
+  size_t nbad = 0, bad = 0;
+  for (size_t i = 0; i < n; i += 7) {
+    exp[32 * i + rng() % 32] ^= 0x40;
+    ++bad;
+  }
+  CHECK(cir_verify_blocks(ctx, ht, arena.data(), off.data(), len.data(), n, exp.data(), ok.data(),
+                          &nbad) == 0);
+  CHECK(nbad == bad);
+  for (size_t i = 0; i < n; ++i) CHECK(ok[i] == (i % 7 != 0));
+  // the asynchronous verify: some polled, some forgotten, the rest awaited
+  const size_t k = std::min<size_t>(n, 64);
+  std::vector<uint64_t> t(k);
+  for (size_t i = 0; i < k; ++i)
+    CHECK(cir_verify_submit(ctx, ht, arena.data() + off[i], len[i], &exp[32 * i], &t[i]) == 0);
+  for (size_t i = 0; i < k; ++i) {
+    int st = 0;
+    if (i % 5 == 1) {
+      CHECK(cir_verify_forget(ctx, t[i]) == 0);
+      CHECK(cir_verify_poll(ctx, t[i], &st) == CIR_ENOTFOUND);
+    } else if (i % 5 == 2) {
+      do CHECK(cir_verify_poll(ctx, t[i], &st) == 0);
+      while (st == 0);
+      CHECK(st == (i % 7 != 0 ? 1 : 2));
+    } else {
+      CHECK(cir_verify_wait(ctx, t[i], &st) == 0);
+      CHECK(st == (i % 7 != 0));
+    }
+  }
+}
+
+static void memory_and_file(cir_ctx* ctx, int ht, const std::string& dir) {
+  std::vector<uint8_t> blob = random_bytes(rng() % (3 << 20));
+  const uint64_t bs = pick({128, 1000, 4096, 32768, 65539, (1 << 20) + 5, 0xffffffffull});
+  uint8_t* h = nullptr;
+  size_t nh = 0;
+  CHECK(cir_hash_memory_ht(ctx, ht, blob.data(), blob.size(), bs, &h, &nh) == 0);
+  std::vector<uint8_t> want = chunk_digests(ht, blob.data(), blob.size(), bs);
+  CHECK(nh * 32 == want.size() && (nh == 0 || memcmp(h, want.data(), want.size()) == 0));
+  cir_free(h);
+  const std::string p = dir + "/file.bin";
+  FILE* f = fopen(p.c_str(), "wb");
+  CHECK(f && fwrite(blob.data(), 1, blob.size(), f) == blob.size());
+  fclose(f);
+  const size_t skip = blob.empty() ? 0 : rng() % (blob.size() + 1);
+  // (a file that grows regrows its slot to the block form: not at 4 GiB blocks)
+  const bool grow = bs < (1ull << 30) && rng() % 3 == 0;
+  if (grow) setenv("CIR_DEBUG_GROW", std::to_string(rng() % 5000).c_str(), 1);
+  const int fd = open(p.c_str(), O_RDONLY);
+  CHECK(fd >= 0 && lseek(fd, (off_t)skip, SEEK_SET) == (off_t)skip);
+  uint64_t size = 0;
+  h = nullptr;
+  const int rc = cir_hash_file_ht(ctx, ht, fd, bs, &size, &h, &nh);
+  if (grow) unsetenv("CIR_DEBUG_GROW");
+  CHECK(rc == 0);
+  want = chunk_digests(ht, blob.data() + skip, blob.size() - skip, bs);
+  CHECK(size == blob.size() - skip && nh * 32 == want.size() &&
+        (nh == 0 || memcmp(h, want.data(), want.size()) == 0));
+  cir_free(h);
+  // Hashes::check_file at commit: the same digests pass, one changed fails
+  int ok = 0;
+  CHECK(lseek(fd, 0, SEEK_SET) == 0);
+  want = chunk_digests(ht, blob.data(), blob.size(), bs);
+  CHECK(cir_check_file(ctx, ht, fd, bs, want.data(), want.size() / 32, &ok) == 0 && ok == 1);
+  if (!want.empty()) {
+    want[rng() % want.size()] ^= 1;
+    CHECK(lseek(fd, 0, SEEK_SET) == 0);
+    CHECK(cir_check_file(ctx, ht, fd, bs, want.data(), want.size() / 32, &ok) == 0 && ok == 0);
+  }
+  close(fd);
+}
+
+static int collect(void* user, const uint8_t* data, size_t n) {
+  auto* v = static_cast<std::vector<uint8_t>*>(user);
+  v->insert(v->end(), data, data + n);
+  return 0;
+}
+
+static void scan(cir_ctx* ctx, int ht, const std::string& dir, int round) {
+  const std::string root = dir + "/tree" + std::to_string(round);
+  const uint64_t bs = pick({128, 4096, 32768, 65539, (1 << 20) + 5});
+  std::vector<std::string> files;
+  bool empty_dir = false;
+  mkdir(root.c_str(), 0755);
+  for (int d = 0; d < 4; ++d) {
+    const std::string sub = root + "/d" + std::to_string(d);
+    mkdir(sub.c_str(), 0755);
+    const int nf = (int)(rng() % 12);
+    empty_dir |= nf == 0;
+    for (int i = 0; i < nf; ++i) {
+      const std::string p = sub + "/f" + std::to_string(i) + (i % 5 == 3 ? " x" : "");
+      const size_t n = (size_t)pick({0, 1, 127, 128, bs - 1, bs, bs + 1, rng() % 300000});
+      std::vector<uint8_t> b = random_bytes(std::min<size_t>(n, 3 << 20));
+      FILE* f = fopen(p.c_str(), "wb");
+      CHECK(f && fwrite(b.data(), 1, b.size(), f) == b.size());
+      fclose(f);
+      files.push_back(p);
+    }
+  }
+  const char* dirs[1] = {root.c_str()};
+  const char* prefixes[1] = {"/"};
+  const uint32_t threads = (uint32_t)pick({0, 1, 3});
+  uint8_t* index = nullptr;
+  size_t len = 0;
+  CHECK(cir_scan_v1(ctx, dirs, prefixes, 1, bs, ht, threads, &index, &len) == 0);
+  std::vector<uint8_t> streamed;
+  size_t len2 = 0;
+  CHECK(cir_scan_v1_write(ctx, dirs, prefixes, 1, bs, ht, threads, collect, &streamed, &len2) == 0);
+  CHECK(len2 == len && streamed.size() == len && memcmp(streamed.data(), index, len) == 0);
+  uint8_t* again = nullptr;
+  size_t alen = 0;
+  // the rewrite (MutableIndex::to_raw_data) re-emits the same bytes -- but
+  // drops empty directories, as the reference's _emit_dir does
+  // (src/cluster/download.rs:292-294), which the scan lists; either way a
+  // second rewrite changes nothing
+  CHECK(cir_index_rewrite(ctx, index, len, &again, &alen) == 0);
+  CHECK(empty_dir ? alen < len : alen == len && memcmp(again, index, len) == 0);
+  uint8_t* twice = nullptr;
+  size_t tlen = 0;
+  CHECK(cir_index_rewrite(ctx, again, alen, &twice, &tlen) == 0);
+  CHECK(tlen == alen && memcmp(twice, again, alen) == 0);
+  cir_free(twice);
+  cir_free(again);
+  uint8_t id[64];
+  size_t idl = 0;
+  CHECK(cir_index_get_hash(index, len, id, &idl) == 0 && idl == 32);
+  cir_indexes* ix = cir_indexes_new();
+  CHECK(ix != nullptr);
+  uint8_t id2[64];
+  size_t idl2 = 0;
+  CHECK(cir_indexes_register(ix, index, len, id2, &idl2) == 0 && idl2 == 32 &&
+        memcmp(id, id2, 32) == 0);
+  uint8_t* back = nullptr;
+  size_t blen = 0;
+  CHECK(cir_indexes_read(ix, id, 32, &back, &blen) == 0 && blen == len &&
+        memcmp(back, index, len) == 0);
+  cir_free(back);
+  cir_indexes_free(ix);
+  // every block of every file served from the registered directory
+  cir_blocks* bl = cir_blocks_new();
+  CHECK(bl != nullptr);
+  CHECK(cir_blocks_register_dir(bl, root.c_str(), index, len) == 0);
+  for (const std::string& p : files) {
+    FILE* f = fopen(p.c_str(), "rb");
+    std::vector<uint8_t> b(4 << 20);
+    const size_t n = fread(b.data(), 1, b.size(), f);
+    fclose(f);
+    for (uint64_t o = 0; o < n; o += bs) {
+      const size_t k = (size_t)std::min<uint64_t>(bs, n - o);
+      uint8_t h[32];
+      host_digest(ht, b.data() + o, k, h);
+      uint8_t* data = nullptr;
+      size_t dlen = 0;
+      CHECK(cir_blocks_read(bl, h, &data, &dlen) == 0 && dlen == k &&
+            memcmp(data, b.data() + o, k) == 0);
+      cir_free(data);
+    }
+  }
+  cir_blocks_free(bl);
+  // put-file's in-memory blocks
+  std::vector<uint8_t> mem = random_bytes(rng() % (1 << 20));
+  cir_blocks* mb = cir_blocks_new();
+  CHECK(cir_blocks_register_memory_ht(ctx, mb, ht, mem.data(), mem.size(), bs) == 0);
+  CHECK(cir_blocks_len(mb) <= (mem.size() + bs - 1) / bs);
+  cir_blocks_free(mb);
+  cir_free(index);
+}
+
+int main(int argc, char** argv) {
+  const int rounds = argc > 1 ? atoi(argv[1]) : 40;
+  rng.seed(argc > 2 ? strtoull(argv[2], nullptr, 10) : 1);
+  char tmpl[] = "/tmp/cir_asan_XXXXXX";
+  const char* dir = mkdtemp(tmpl);
+  if (!dir) return 2;
+  cir_ctx* ctx[3] = {nullptr, nullptr, nullptr};
+  if (cir_init_n(&ctx[0], 1u, 1 << 20, 0, 0)) {
+    fprintf(stderr, "cir_init: %s\n", cir_last_error());
+    return 2;
+  }
+  setenv("CIR_DEBUG_SPLIT", "3", 1);
+  const int rc1 = cir_init_n(&ctx[1], 1u, 1000003, 0, 0);
+  unsetenv("CIR_DEBUG_SPLIT");
+  if (rc1 || cir_init_n(&ctx[2], 1u, 1 << 20, 0, CIR_INIT_ONE_SHOT)) {
+    fprintf(stderr, "cir_init: %s\n", cir_last_error());
+    return 2;
+  }
+  for (int r = 0; r < rounds && !g_fail; ++r) {
+    cir_ctx* c = ctx[r % 3];
+    const int ht = rng() % 4 == 0 ? CIR_HASH_SHA512_256 : CIR_HASH_BLAKE2B_256;
+    cir_set_footer_mode(c, rng() % 2 ? CIR_FOOTER_GPU : CIR_FOOTER_HOST);
+    descriptors(c, ht);
+    memory_and_file(c, ht, dir);
+    scan(c, ht, dir, r);
+    fprintf(stderr, "round %d ok (context %d, hash type %d)\n", r, r % 3, ht);
+  }
+  uint8_t one[32], want[32];
+  std::vector<uint8_t> blk = random_bytes(32768);
+  if (cir_blake2b256(blk.data(), blk.size(), one) != 0) ++g_fail;
+  host_digest(CIR_HASH_BLAKE2B_256, blk.data(), blk.size(), want);
+  if (memcmp(one, want, 32) != 0) ++g_fail;
+  for (cir_ctx* c : ctx) cir_destroy(c);
+  std::string rm = std::string("rm -rf ") + dir;
+  if (system(rm.c_str()) != 0) fprintf(stderr, "could not remove %s\n", dir);
+  printf("%s %d rounds\n", g_fail ? "FAIL" : "ok", rounds);
+  return g_fail ? 1 : 0;
+}
