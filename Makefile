@@ -22,7 +22,7 @@ OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS_HIP)) \
         $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(SRCS_CPP))
 HDRS := $(wildcard $(CSRC)/*.hpp) include/ciruela_blockhash.h
 
-all: $(LIB) $(CLI) build/hash_bytes_conc build/verify_daemon_sim build/host_asan_driver oracle
+all: $(LIB) $(CLI) build/hash_bytes_conc build/verify_daemon_sim build/host_asan_driver build/host_tsan_driver oracle
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -68,6 +68,20 @@ build/asan/host_asan_driver.o: tools/host_asan_driver.cpp include/ciruela_blockh
 build/host_asan_driver: $(ASAN_OBJS)
 	$(HIPCC) $(HIPFLAGS) $(ASAN_HOST) -o $@ $(ASAN_OBJS) -lpthread
 asan: build/host_asan_driver
+
+# the same driver with the host code under ThreadSanitizer
+# (TSAN_OPTIONS=suppressions=tools/tsan_hip.supp)
+TSAN_HOST := -O1 -g -Xarch_host -fsanitize=thread
+TSAN_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS_HIP)) \
+             $(patsubst $(CSRC)/%.cpp,build/tsan/%.o,$(SRCS_CPP)) build/tsan/host_asan_driver.o
+build/tsan/%.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p build/tsan
+	$(HIPCC) $(HOSTFLAGS) $(TSAN_HOST) -c $< -o $@
+build/tsan/host_asan_driver.o: tools/host_asan_driver.cpp include/ciruela_blockhash.h
+	@mkdir -p build/tsan
+	$(HIPCC) $(HOSTFLAGS) $(TSAN_HOST) -c $< -o $@
+build/host_tsan_driver: $(TSAN_OBJS)
+	$(HIPCC) $(HIPFLAGS) $(TSAN_HOST) -o $@ $(TSAN_OBJS) -lpthread
 
 oracle:
 	$(MAKE) -C oracle

@@ -10,8 +10,11 @@
 // types, batch verify with wrong digests, hash_memory and hash_file at block
 // sizes up to 2^32-1 (a file that grows, CIR_DEBUG_GROW), the asynchronous
 // verify with forgets, scans returned whole and written out as they go,
-// the rewrite, and the registries.  Any memory error or undefined behaviour
-// ends the run with the sanitizer's report.
+// the rewrite, and the registries; every fifth round four more threads call
+// into the same context at once.  Any memory error or undefined behaviour
+// ends the run with the sanitizer's report.  The same source builds under
+// ThreadSanitizer (make build/host_tsan_driver; tools/tsan_hip.supp drops
+// the reports inside the uninstrumented HIP and HSA runtimes).
 //   build/host_asan_driver [rounds=40] [seed=1]
 //   (ASAN_OPTIONS=detect_leaks=0: the HIP runtime keeps its allocations)
 #include <fcntl.h>
@@ -21,13 +24,15 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ciruela_blockhash.h"
 
-static int g_fail = 0;
+static std::atomic<int> g_fail{0};
 #define CHECK(c)                                                                     \
   do {                                                                               \
     if (!(c)) {                                                                      \
@@ -37,7 +42,7 @@ static int g_fail = 0;
     }                                                                                \
   } while (0)
 
-static std::mt19937_64 rng;
+static thread_local std::mt19937_64 rng;
 static uint64_t pick(std::initializer_list<uint64_t> v) {
   return v.begin()[rng() % v.size()];
 }
@@ -110,7 +115,7 @@ static void descriptors(cir_ctx* ctx, int ht) {
   }
 }
 
-static void memory_and_file(cir_ctx* ctx, int ht, const std::string& dir) {
+static void memory_and_file(cir_ctx* ctx, int ht, const std::string& dir, int who = 0) {
   std::vector<uint8_t> blob = random_bytes(rng() % (3 << 20));
   const uint64_t bs = pick({128, 1000, 4096, 32768, 65539, (1 << 20) + 5, 0xffffffffull});
   uint8_t* h = nullptr;
@@ -119,13 +124,15 @@ static void memory_and_file(cir_ctx* ctx, int ht, const std::string& dir) {
   std::vector<uint8_t> want = chunk_digests(ht, blob.data(), blob.size(), bs);
   CHECK(nh * 32 == want.size() && (nh == 0 || memcmp(h, want.data(), want.size()) == 0));
   cir_free(h);
-  const std::string p = dir + "/file.bin";
+  const std::string p = dir + "/file" + std::to_string(who) + ".bin";
   FILE* f = fopen(p.c_str(), "wb");
   CHECK(f && fwrite(blob.data(), 1, blob.size(), f) == blob.size());
   fclose(f);
   const size_t skip = blob.empty() ? 0 : rng() % (blob.size() + 1);
   // (a file that grows regrows its slot to the block form: not at 4 GiB blocks)
-  const bool grow = bs < (1ull << 30) && rng() % 3 == 0;
+  // (the environment is set from the driving thread only: setenv is not
+  // safe beside other threads' getenv)
+  const bool grow = who == 0 && bs < (1ull << 30) && rng() % 3 == 0;
   if (grow) setenv("CIR_DEBUG_GROW", std::to_string(rng() % 5000).c_str(), 1);
   const int fd = open(p.c_str(), O_RDONLY);
   CHECK(fd >= 0 && lseek(fd, (off_t)skip, SEEK_SET) == (off_t)skip);
@@ -265,13 +272,27 @@ int main(int argc, char** argv) {
     fprintf(stderr, "cir_init: %s\n", cir_last_error());
     return 2;
   }
-  for (int r = 0; r < rounds && !g_fail; ++r) {
+  for (int r = 0; r < rounds && !g_fail.load(); ++r) {
     cir_ctx* c = ctx[r % 3];
     const int ht = rng() % 4 == 0 ? CIR_HASH_SHA512_256 : CIR_HASH_BLAKE2B_256;
     cir_set_footer_mode(c, rng() % 2 ? CIR_FOOTER_GPU : CIR_FOOTER_HOST);
     descriptors(c, ht);
     memory_and_file(c, ht, dir);
     scan(c, ht, dir, r);
+    if (r % 5 == 4) {
+      // callers on several threads at once on the same context (every entry
+      // point is thread-safe on a context)
+      std::vector<std::thread> th;
+      const uint64_t base = rng();
+      for (int w = 1; w <= 4; ++w)
+        th.emplace_back([&, w] {
+          rng.seed(base + (uint64_t)w);
+          const int wht = w % 3 == 0 ? CIR_HASH_SHA512_256 : CIR_HASH_BLAKE2B_256;
+          descriptors(c, wht);
+          memory_and_file(c, wht, dir, w);
+        });
+      for (auto& t : th) t.join();
+    }
     fprintf(stderr, "round %d ok (context %d, hash type %d)\n", r, r % 3, ht);
   }
   uint8_t one[32], want[32];
@@ -282,6 +303,12 @@ int main(int argc, char** argv) {
   for (cir_ctx* c : ctx) cir_destroy(c);
   std::string rm = std::string("rm -rf ") + dir;
   if (system(rm.c_str()) != 0) fprintf(stderr, "could not remove %s\n", dir);
-  printf("%s %d rounds\n", g_fail ? "FAIL" : "ok", rounds);
-  return g_fail ? 1 : 0;
+  printf("%s %d rounds\n", g_fail.load() ? "FAIL" : "ok", rounds);
+  fflush(stdout);
+  fflush(stderr);
+  // (the contexts are destroyed above; the HIP runtime's own exit handlers
+  // free memory after ASan's device-allocator hooks are gone and trip its
+  // CHECK now and then -- not this library's code, so skipped, as the CLI
+  // skips them)
+  _exit(g_fail.load() ? 1 : 0);
 }
