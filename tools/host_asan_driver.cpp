@@ -9,7 +9,8 @@
 // against the oracle in the CPU suite): descriptor batches in both hash
 // types, batch verify with wrong digests, hash_memory and hash_file at block
 // sizes up to 2^32-1 (a file that grows, CIR_DEBUG_GROW), the asynchronous
-// verify with forgets, scans returned whole and written out as they go,
+// verify with forgets, the device-resident entry points on a stream of the
+// caller's, scans returned whole and written out as they go,
 // the rewrite, and the registries; every fifth round four more threads call
 // into the same context at once.  Any memory error or undefined behaviour
 // ends the run with the sanitizer's report.  The same source builds under
@@ -29,6 +30,8 @@
 #include <string>
 #include <thread>
 #include <vector>
+
+#include <hip/hip_runtime.h>
 
 #include "ciruela_blockhash.h"
 
@@ -158,6 +161,66 @@ static void memory_and_file(cir_ctx* ctx, int ht, const std::string& dir, int wh
   close(fd);
 }
 
+// the device-resident entry points: a file's blocks (cir_hash_chunks_dev,
+// with the relayed / quad rest when the shape calls for it), a descriptor
+// batch and a device verify, on a stream of the caller's
+static void device_paths(cir_ctx* ctx, int ht) {
+  const uint64_t bs = pick({1024, 4096, 32768});
+  const uint64_t nbytes = bs * pick({1, 257, 1500}) + rng() % bs;
+  std::vector<uint8_t> host = random_bytes(nbytes);
+  uint8_t *d_data = nullptr, *d_out = nullptr;
+  hipStream_t st = nullptr;
+  CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess);
+  const uint64_t nblk = (nbytes + bs - 1) / bs;
+  CHECK(hipMalloc(&d_data, nbytes + 64) == hipSuccess && hipMalloc(&d_out, 32 * nblk + 64) == hipSuccess);
+  CHECK(hipMemcpy(d_data, host.data(), nbytes, hipMemcpyHostToDevice) == hipSuccess);
+  std::vector<uint8_t> got(32 * nblk);
+  if (ht == CIR_HASH_BLAKE2B_256) {
+    CHECK(cir_hash_chunks_dev(ctx, d_data, nbytes, bs, d_out, st) == 0);
+    CHECK(hipStreamSynchronize(st) == hipSuccess);
+    CHECK(hipMemcpy(got.data(), d_out, got.size(), hipMemcpyDeviceToHost) == hipSuccess);
+    CHECK(got == chunk_digests(ht, host.data(), nbytes, bs));
+  }
+  // the same bytes as descriptors, every third block cut short
+  std::vector<uint64_t> off(nblk);
+  std::vector<uint32_t> len(nblk);
+  for (uint64_t b = 0; b < nblk; ++b) {
+    off[b] = b * bs;
+    const uint64_t full = std::min<uint64_t>(bs, nbytes - b * bs);
+    len[b] = (uint32_t)(full - (b % 3 == 1 ? rng() % std::min<uint64_t>(100, full + 1) : 0));
+  }
+  // (the kernels trust device descriptors: check them here, before a launch)
+  for (uint64_t b = 0; b < nblk; ++b) CHECK(off[b] + len[b] <= nbytes);
+  uint64_t* d_off = nullptr;
+  uint32_t* d_len = nullptr;
+  uint8_t *d_exp = nullptr, *d_dig = nullptr, *d_ok = nullptr;
+  uint32_t* d_nbad = nullptr;
+  CHECK(hipMalloc(&d_off, 8 * nblk) == hipSuccess && hipMalloc(&d_len, 4 * nblk) == hipSuccess &&
+        hipMalloc(&d_exp, 32 * nblk) == hipSuccess && hipMalloc(&d_dig, 32 * nblk) == hipSuccess &&
+        hipMalloc(&d_ok, nblk) == hipSuccess && hipMalloc(&d_nbad, 4) == hipSuccess);
+  CHECK(hipMemcpy(d_off, off.data(), 8 * nblk, hipMemcpyHostToDevice) == hipSuccess);
+  CHECK(hipMemcpy(d_len, len.data(), 4 * nblk, hipMemcpyHostToDevice) == hipSuccess);
+  CHECK(cir_hash_blocks_dev_ht(ctx, ht, d_data, d_off, d_len, nblk, d_out, st) == 0);
+  CHECK(hipStreamSynchronize(st) == hipSuccess);
+  CHECK(hipMemcpy(got.data(), d_out, got.size(), hipMemcpyDeviceToHost) == hipSuccess);
+  std::vector<uint8_t> want(32 * nblk);
+  for (uint64_t b = 0; b < nblk; ++b) host_digest(ht, host.data() + off[b], len[b], &want[32 * b]);
+  CHECK(got == want);
+  want[32 * (nblk - 1)] ^= 2;
+  CHECK(hipMemcpy(d_exp, want.data(), want.size(), hipMemcpyHostToDevice) == hipSuccess);
+  CHECK(cir_verify_blocks_dev(ctx, ht, d_data, d_off, d_len, nblk, d_exp, d_dig, d_ok, d_nbad, st) == 0);
+  CHECK(hipStreamSynchronize(st) == hipSuccess);
+  uint32_t nbad = 0;
+  std::vector<uint8_t> ok(nblk);
+  CHECK(hipMemcpy(&nbad, d_nbad, 4, hipMemcpyDeviceToHost) == hipSuccess);
+  CHECK(hipMemcpy(ok.data(), d_ok, nblk, hipMemcpyDeviceToHost) == hipSuccess);
+  CHECK(nbad == 1 && ok[nblk - 1] == 0 && (nblk == 1 || ok[0] == 1));
+  for (void* p : {(void*)d_data, (void*)d_out, (void*)d_off, (void*)d_len, (void*)d_exp, (void*)d_dig,
+                  (void*)d_ok, (void*)d_nbad})
+    (void)hipFree(p);
+  (void)hipStreamDestroy(st);
+}
+
 static int collect(void* user, const uint8_t* data, size_t n) {
   auto* v = static_cast<std::vector<uint8_t>*>(user);
   v->insert(v->end(), data, data + n);
@@ -279,6 +342,7 @@ int main(int argc, char** argv) {
     descriptors(c, ht);
     memory_and_file(c, ht, dir);
     scan(c, ht, dir, r);
+    device_paths(c, ht);
     if (r % 5 == 4) {
       // callers on several threads at once on the same context (every entry
       // point is thread-safe on a context)
