@@ -101,6 +101,13 @@ class Context:
         except Exception:
             pass
 
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
     # ---- device-resident entry points (pointers are device addresses) ----
     def hash_chunks_dev(self, d_data, nbytes, block_size, d_out, stream=0):
         _n.check(_n.lib.cir_hash_chunks_dev(self._h, d_data, nbytes, block_size, d_out, stream))

@@ -639,7 +639,13 @@ def test_one_shot_context(gpu, oracle, tmp_path):
     part behind the lane part on the one stream, no relay), a ragged file on
     the device, host batches over several slots (allocated on demand), a scan
     with the GPU footer (its chain stream created on demand) and verify."""
-    c = gpu.Context(device_mask=1, staging_bytes=1 << 20, one_shot=True)
+    with gpu.Context(device_mask=1, staging_bytes=1 << 20, one_shot=True) as c:
+        one_shot_paths(gpu, c, oracle, tmp_path)
+    with pytest.raises(gpu.CiruelaError):  # closed: the handle is gone
+        c.hash_memory(b"x", 4096)
+
+
+def one_shot_paths(gpu, c, oracle, tmp_path):
     test_desc_mixed_ragged_shuffled(gpu, c, oracle)
     test_desc_large_batch_exclusive_quad(gpu, c, oracle)
     test_chunks_dev_vs_oracle(gpu, c, oracle, 32768, 32768 * 4099 + 77)
@@ -663,7 +669,6 @@ def test_one_shot_context(gpu, oracle, tmp_path):
         cfg = gpu.ScannerConfig.new().block_size(32768)
         cfg.add_dir(str(root), "/")
         assert gpu.v1.scan(cfg, context=c) == dirsig_oracle.scan(str(root), 32768, "blake2b/256")
-    c.close()
 
 
 def test_sha512_256_single_and_batches(gpu, ctx, oracle):
