@@ -547,6 +547,40 @@ def test_cli_sync(gpu, tmp_path, teardown):
     assert b"Indexed" in p.stderr
 
 
+def test_cli_sync_several_jobs(gpu, tmp_path):
+    """Several `--append` / `--append-weak` / `--replace` jobs in one
+    `ciruela-index sync` (src/client/sync/mod.rs:168-220 walks its uploads
+    the same way): one line per job in order, each index the scan oracle's
+    for its own directory, a block size given with --block-size, a one-shot
+    context for the jobs' total input (CIR_TRACE)."""
+    import subprocess
+    from conftest import ROOT
+    rng = random.Random(0xC11)
+    srcs = []
+    for k in range(3):
+        d = tmp_path / ("src%d" % k)
+        d.mkdir()
+        for i in range(rng.randrange(1, 8)):
+            (d / ("f%d" % i)).write_bytes(rng.randbytes(rng.randrange(0, 200000)))
+        srcs.append(d)
+    args = [os.path.join(ROOT, "bin", "ciruela-index"), "sync", "--block-size", "65536",
+            "--append", "%s:/a" % srcs[0], "--append-weak", "%s:/b/c" % srcs[1],
+            "--replace", "%s:/d" % srcs[2], "--index-dir", str(tmp_path)]
+    p = subprocess.run(args, env=dict(os.environ, CIR_TRACE="1"), capture_output=True,
+                       timeout=120)
+    assert p.returncode == 0, p.stderr
+    lines = [ln.split() for ln in p.stdout.decode().splitlines()]
+    assert [(ln[1], ln[2], ln[3]) for ln in lines] == [
+        ("append", "/a", str(srcs[0])), ("append-weak", "/b/c", str(srcs[1])),
+        ("replace", "/d", str(srcs[2]))]
+    for ln, src in zip(lines, srcs):
+        want = dirsig_oracle.scan(str(src), 65536)
+        assert (tmp_path / (ln[0] + ".ds1")).read_bytes() == want
+        assert want.endswith(ln[0].encode() + b"\n")
+    assert p.stderr.count(b"Indexed") == 3
+    assert b"1 device(s) for" in p.stderr
+
+
 def test_cli_exits_normally_under_a_profiler(gpu, tmp_path):
     """With a profiler's environment (ROCPROF_* / ROCP_TOOL_LIBRARIES, as
     rocprofv3 sets for its tool library) `ciruela-index` skips cir_destroy
