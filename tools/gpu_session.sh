@@ -45,6 +45,13 @@ for s in "$@"; do
       step cli 120 ./bin/ciruela-index hash /tmp/cli_probe.bin ;;
     smoke)
       step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    sanitizers)  # the host code under ASan + UBSan and under TSan (make builds both drivers)
+      ASAN_OPTIONS=detect_leaks=0:verify_asan_link_order=0 step asan 400 \
+        ./build/host_asan_driver "${SAN_ROUNDS:-60}" "${SAN_SEED:-1}" > gpurun_out/asan.out 2> gpurun_out/asan.err
+      TSAN_OPTIONS="suppressions=tools/tsan_hip.supp report_thread_leaks=0" step tsan 600 \
+        ./build/host_tsan_driver "${SAN_ROUNDS:-30}" "${SAN_SEED:-1}" > gpurun_out/tsan.out 2> gpurun_out/tsan.err
+      cat gpurun_out/asan.out gpurun_out/tsan.out
+      echo "tsan warnings: $(grep -c 'WARNING: ThreadSanitizer' gpurun_out/tsan.err)" ;;
     tests)
       step tests 1100 python -u -m pytest tests -v -m gpu -x -p no:cacheprovider \
         --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} \
