@@ -186,8 +186,14 @@ static int walk(const std::string& real, const std::string& vpath, unsigned thre
       }
       lk.lock();
       --busy;
-      if (n->rc == CIR_OK)
-        for (auto& c : n->subdirs) queue.push_back(c.get());
+      if (n->rc == CIR_OK) {
+        try {
+          for (auto& c : n->subdirs) queue.push_back(c.get());
+        } catch (...) {  // (the others must still be woken below)
+          n->rc = CIR_ENOMEM;
+          n->err = "walking " + n->real + ": out of memory";
+        }
+      }
       cv.notify_all();
     }
   });
