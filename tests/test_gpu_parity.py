@@ -1321,6 +1321,36 @@ def test_error_paths_are_codes_not_aborts(gpu, small_ctx, tmp_path):
 
 
 @pytest.mark.skipif(os.geteuid() == 0, reason="root reads files whatever their mode")
+def test_scan_reports_the_first_failure_in_walk_order(gpu, small_ctx, tmp_path):
+    """The walk reads directories in parallel but reports a failure as the
+    serial, depth-first walk meets it first: of 40 unreadable directories
+    the first by name (d00, under a tree whose other branches are read
+    first or at the same time), every time."""
+    n = gpu._n
+    for k in range(40):
+        d = tmp_path / "t" / ("d%02d" % k)
+        (d / "sub").mkdir(parents=True)
+        (d / "sub" / "f").write_bytes(b"x" * k)
+    for k in range(8):
+        (tmp_path / "t" / ("a%d" % k)).mkdir()
+        for i in range(50):
+            (tmp_path / "t" / ("a%d" % k) / ("f%02d" % i)).write_bytes(b"y")
+    locked = [tmp_path / "t" / ("d%02d" % k) / "sub" for k in range(40)]
+    for d in locked:
+        os.chmod(d, 0)
+    try:
+        cfg = gpu.ScannerConfig.new().threads(8).add_dir(str(tmp_path / "t"), "/")
+        for _ in range(5):
+            with pytest.raises(n.CiruelaError) as e:
+                gpu.v1.scan(cfg, context=small_ctx)
+            assert e.value.status == n.CIR_EIO
+            assert str(locked[0]) in str(e.value), e.value
+    finally:
+        for d in locked:
+            os.chmod(d, 0o755)
+
+
+@pytest.mark.skipif(os.geteuid() == 0, reason="root reads files whatever their mode")
 @pytest.mark.parametrize("what", ["file", "dir"])
 def test_scan_unreadable_entry_is_an_io_error(gpu, small_ctx, tmp_path, what):
     """v1::scan returns io::Error for a file or directory it cannot read
