@@ -1,6 +1,9 @@
 # Build of the MI355X block-hash path (gfx950 only) and of the CPU oracle.
-#   make            -> ciruela_amd/libciruela_amd.so, bin/ciruela-index, oracle
+#   make            -> ciruela_amd/libciruela_amd.so, bin/ciruela-index, the two
+#                      load drivers under build/, oracle
 #   make oracle     -> oracle/build/liboracle_blake2b.so (test infrastructure)
+#   make asan/tsan  -> build/host_{asan,tsan}_driver (host code under the
+#                      sanitizers; `make sanitizers` = both; not in `all`)
 HIPCC ?= /opt/rocm/bin/hipcc
 CXX ?= g++
 CC ?= gcc
@@ -22,7 +25,7 @@ OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS_HIP)) \
         $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(SRCS_CPP))
 HDRS := $(wildcard $(CSRC)/*.hpp) include/ciruela_blockhash.h
 
-all: $(LIB) $(CLI) build/hash_bytes_conc build/verify_daemon_sim build/host_asan_driver build/host_tsan_driver oracle
+all: $(LIB) $(CLI) build/hash_bytes_conc build/verify_daemon_sim oracle
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -82,6 +85,9 @@ build/tsan/host_asan_driver.o: tools/host_asan_driver.cpp include/ciruela_blockh
 	$(HIPCC) $(HOSTFLAGS) $(TSAN_HOST) -c $< -o $@
 build/host_tsan_driver: $(TSAN_OBJS)
 	$(HIPCC) $(HIPFLAGS) $(TSAN_HOST) -o $@ $(TSAN_OBJS) -lpthread
+tsan: build/host_tsan_driver
+
+sanitizers: asan tsan
 
 oracle:
 	$(MAKE) -C oracle
@@ -90,4 +96,4 @@ clean:
 	rm -rf build $(LIB) $(CLI)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean asan
+.PHONY: all oracle clean asan tsan sanitizers

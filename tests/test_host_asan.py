@@ -1,6 +1,6 @@
 """The library's host code under AddressSanitizer + UBSan, and under
-ThreadSanitizer, on the GPU (tools/host_asan_driver.cpp, built by `make`
-twice with the sanitizers on the host translation units only, against the
+ThreadSanitizer, on the GPU (tools/host_asan_driver.cpp, built by `make asan` and
+`make tsan` with the sanitizers on the host translation units only, against the
 production device code): random rounds
 of every host-path entry point -- descriptor batches, batch and asynchronous
 verify, hash_memory / hash_file / check_file at block sizes up to 2^32-1
@@ -22,7 +22,7 @@ from conftest import ROOT
 @pytest.mark.gpu
 def test_host_code_under_asan_and_ubsan():
     exe = os.path.join(ROOT, "build", "host_asan_driver")
-    assert os.path.exists(exe), "build/host_asan_driver missing: run make"
+    assert os.path.exists(exe), "build/host_asan_driver missing: run make asan"
     # leaks: the HIP runtime keeps allocations to the end; link order: the
     # sanitizer runtime is linked into the executable, not preloaded
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:verify_asan_link_order=0",
@@ -35,7 +35,7 @@ def test_host_code_under_asan_and_ubsan():
 @pytest.mark.gpu
 def test_host_code_under_tsan():
     exe = os.path.join(ROOT, "build", "host_tsan_driver")
-    assert os.path.exists(exe), "build/host_tsan_driver missing: run make"
+    assert os.path.exists(exe), "build/host_tsan_driver missing: run make tsan"
     supp = os.path.join(ROOT, "tools", "tsan_hip.supp")
     env = dict(os.environ, TSAN_OPTIONS="suppressions=%s report_thread_leaks=0" % supp)
     p = subprocess.run([exe, "15", "5"], capture_output=True, timeout=300, env=env)
