@@ -117,6 +117,14 @@ class Context:
         _n.check(_n.lib.cir_hash_blocks_dev_ht(self._h, ht, d_arena, d_off, d_len, nblk, d_out,
                                                stream))
 
+    def hash_blocks_dev_bounded(self, d_arena, arena_bytes, d_off, d_len, nblk, d_out,
+                                d_nrange=0, stream=0, hash_type=None):
+        """hash_blocks_dev over untrusted descriptors: a block past
+        arena_bytes is not read, its digest is zeros, *d_nrange counts them."""
+        ht = (hash_type or HashType.blake2b_256()).code
+        _n.check(_n.lib.cir_hash_blocks_dev_bounded(self._h, ht, d_arena, arena_bytes, d_off,
+                                                    d_len, nblk, d_out, d_nrange, stream))
+
     # ---- host-memory entry points ----------------------------------------
     def hash_blocks(self, arena, offsets, lengths, hash_type=None):
         """Digests (n x 32 bytes) of arena[off[i] : off[i] + len[i]]."""
@@ -194,6 +202,15 @@ class Context:
         ht = (hash_type or HashType.blake2b_256()).code
         _n.check(_n.lib.cir_verify_blocks_dev(self._h, ht, d_arena, d_off, d_len, nblk,
                                               d_expected, d_digests, d_ok, d_nbad, stream))
+
+    def verify_blocks_dev_bounded(self, d_arena, arena_bytes, d_off, d_len, nblk, d_expected,
+                                  d_digests, d_ok=0, d_nbad=0, stream=0, hash_type=None):
+        """verify_blocks_dev over untrusted descriptors: a block past
+        arena_bytes is not read and counts as a mismatch."""
+        ht = (hash_type or HashType.blake2b_256()).code
+        _n.check(_n.lib.cir_verify_blocks_dev_bounded(self._h, ht, d_arena, arena_bytes, d_off,
+                                                      d_len, nblk, d_expected, d_digests, d_ok,
+                                                      d_nbad, stream))
 
     # ---- asynchronous per-block verify (FetchBlock::poll, fetch_blocks.rs:77)
     def verify_submit(self, data, expected, hash_type=None):

@@ -114,6 +114,11 @@ _SIGS = {
                                              c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cir_verify_blocks": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, c_vp, c_vp, ctypes.c_size_t,
                                          c_vp, c_vp, c_sizep]),
+    "cir_hash_blocks_dev_bounded": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, ctypes.c_uint64, c_vp,
+                                                   c_vp, ctypes.c_size_t, c_vp, c_vp, c_vp]),
+    "cir_verify_blocks_dev_bounded": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, ctypes.c_uint64,
+                                                     c_vp, c_vp, ctypes.c_size_t, c_vp, c_vp, c_vp,
+                                                     c_vp, c_vp]),
     "cir_check_file": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, c_vp,
                                       ctypes.c_size_t, ctypes.POINTER(ctypes.c_int)]),
     "cir_debug_compress_only_dev": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, c_vp, c_vp]),

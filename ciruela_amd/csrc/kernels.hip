@@ -1055,7 +1055,8 @@ hipError_t launch_compress_only(uint64_t nlanes, uint32_t lines, uint8_t* out, h
 // Daemon-side verify (fetch_blocks.rs:77 `hash_bytes(&data) == blk.hash`):
 // one lane per digest, mismatches counted per wave with a ballot.
 __global__ void k_verify(const uint8_t* __restrict__ got, const uint8_t* __restrict__ want,
-                         uint64_t n, uint8_t* __restrict__ ok, uint32_t* __restrict__ nbad) {
+                         uint64_t n, uint8_t* __restrict__ ok, uint32_t* __restrict__ nbad,
+                         const uint8_t* __restrict__ flag) {
   const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool bad = false;
   if (b < n) {
@@ -1064,7 +1065,7 @@ __global__ void k_verify(const uint8_t* __restrict__ got, const uint8_t* __restr
     const uint4 g0 = g[0], g1 = g[1], w0 = w[0], w1 = w[1];
     const uint32_t diff = (g0.x ^ w0.x) | (g0.y ^ w0.y) | (g0.z ^ w0.z) | (g0.w ^ w0.w) |
                           (g1.x ^ w1.x) | (g1.y ^ w1.y) | (g1.z ^ w1.z) | (g1.w ^ w1.w);
-    bad = diff != 0;
+    bad = diff != 0 || (flag && flag[b]);
     if (ok) ok[b] = bad ? 0 : 1;
   }
   const uint64_t mask = __ballot(bad);
@@ -1072,10 +1073,10 @@ __global__ void k_verify(const uint8_t* __restrict__ got, const uint8_t* __restr
 }
 
 hipError_t launch_verify(const uint8_t* got, const uint8_t* want, uint64_t n, uint8_t* ok,
-                         uint32_t* nbad, hipStream_t s) {
+                         uint32_t* nbad, hipStream_t s, const uint8_t* flag) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_verify, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, got, want, n,
-                     ok, nbad);
+                     ok, nbad, flag);
   return hipGetLastError();
 }
 

@@ -104,6 +104,18 @@ constexpr uint32_t kLaneChainCost = 4;
 hipError_t launch_order_desc(const uint32_t* len, uint64_t n, void* scratch, size_t bytes,
                              uint32_t** perm, uint32_t** n_long, hipStream_t s);
 
+// Bounds of an untrusted descriptor batch (order.hip): in `scratch`
+// (bound_scratch_bytes(n) bytes of device memory) *slen = the lengths with
+// every out-of-range block's set to 0 (off + len wraps or passes
+// arena_bytes), *flag = 1 per out-of-range block; *nflag (device u32, zeroed
+// here; NULL: a counter inside the scratch) = their number.
+size_t bound_scratch_bytes(uint64_t n);
+hipError_t launch_desc_bound(const uint64_t* off, const uint32_t* len, uint64_t n,
+                             uint64_t arena_bytes, void* scratch, uint32_t* nflag,
+                             uint32_t** slen, uint8_t** flag, hipStream_t s);
+// out + 32 b = 32 zero bytes for every flagged block b.
+hipError_t launch_desc_zero(const uint8_t* flag, uint64_t n, uint8_t* out, hipStream_t s);
+
 // SHA-512/256 per descriptor (one lane per block), digest b -> out + 32 b.
 hipError_t launch_sha_desc(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
                            const uint32_t* perm, uint64_t n, uint8_t* out, hipStream_t s);
@@ -124,8 +136,9 @@ hipError_t launch_single(const uint8_t* h_src, uint32_t n, uint8_t* d_scratch, u
 
 // Compare n digests (32 B each, both 16-B aligned) with the expected ones:
 // ok[b] = 1 / 0 (ok may be null); *nbad += mismatches (nbad may be null).
+// flag (nullable): a flagged block is a mismatch whatever its digest.
 hipError_t launch_verify(const uint8_t* got, const uint8_t* want, uint64_t n, uint8_t* ok,
-                         uint32_t* nbad, hipStream_t s);
+                         uint32_t* nbad, hipStream_t s, const uint8_t* flag = nullptr);
 
 // nlanes x `lines` register-only compressions (diagnostic VALU ceiling).
 hipError_t launch_compress_only(uint64_t nlanes, uint32_t lines, uint8_t* out, hipStream_t s);

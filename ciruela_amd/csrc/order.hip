@@ -156,6 +156,79 @@ size_t order_scratch_bytes(uint64_t n) {
   return kHead + 2 * arr;
 }
 
+// ---- bounds of an untrusted descriptor batch ------------------------------
+// The *_dev_bounded entry points take descriptors from another party's data
+// (the daemon's received blocks, fetch_blocks.rs:77): block i is in range
+// when off[i] + len[i] neither wraps nor passes arena_bytes.  One pass over
+// the descriptors writes the lengths the hash kernels then read: len[i] for
+// a block in range, 0 for one out of range -- a zero-length chain reads
+// nothing (every loader reads at most its n bytes), so no kernel touches
+// memory outside the arena -- and flags the out-of-range ones.
+
+__global__ __launch_bounds__(256) void k_desc_bound(const uint64_t* __restrict__ off,
+                                                    const uint32_t* __restrict__ len, uint64_t n,
+                                                    uint64_t arena_bytes,
+                                                    uint32_t* __restrict__ slen,
+                                                    uint8_t* __restrict__ flag,
+                                                    uint32_t* __restrict__ nflag) {
+  uint32_t bad_here = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t o = off[i];
+    const uint32_t l = len[i];
+    const uint64_t end = o + l;
+    const bool bad = end < o || end > arena_bytes;
+    slen[i] = bad ? 0u : l;
+    flag[i] = bad ? 1 : 0;
+    bad_here += bad;
+  }
+#pragma unroll
+  for (int sft = 1; sft < 64; sft <<= 1) bad_here += (uint32_t)__shfl_xor((int)bad_here, sft);
+  if ((threadIdx.x & 63u) == 0 && bad_here) atomicAdd(nflag, bad_here);
+}
+
+// Digests of the flagged blocks: 32 zero bytes (the hash kernels wrote the
+// empty input's digest there).
+__global__ __launch_bounds__(256) void k_desc_zero(const uint8_t* __restrict__ flag, uint64_t n,
+                                                   uint8_t* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    if (flag[i]) {
+      uint4* o = reinterpret_cast<uint4*>(out + 32 * i);
+      o[0] = make_uint4(0, 0, 0, 0);
+      o[1] = make_uint4(0, 0, 0, 0);
+    }
+}
+
+size_t bound_scratch_bytes(uint64_t n) {
+  const uint64_t arr = (n * 4 + 255) & ~(uint64_t)255;
+  return 256 + arr + ((n + 255) & ~(uint64_t)255);
+}
+
+hipError_t launch_desc_bound(const uint64_t* off, const uint32_t* len, uint64_t n,
+                             uint64_t arena_bytes, void* scratch, uint32_t* nflag,
+                             uint32_t** slen, uint8_t** flag, hipStream_t s) {
+  // scratch: [256 B: an own counter][slen][flag]
+  const uint64_t arr = (n * 4 + 255) & ~(uint64_t)255;
+  uint8_t* base = static_cast<uint8_t*>(scratch);
+  *slen = reinterpret_cast<uint32_t*>(base + 256);
+  *flag = base + 256 + arr;
+  if (!nflag) nflag = reinterpret_cast<uint32_t*>(base);
+  hipError_t e = hipMemsetAsync(nflag, 0, 4, s);
+  if (e != hipSuccess || n == 0) return e;
+  const uint64_t grid = std::min<uint64_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(k_desc_bound, dim3((unsigned)grid), dim3(256), 0, s, off, len, n,
+                     arena_bytes, *slen, *flag, nflag);
+  return hipGetLastError();
+}
+
+hipError_t launch_desc_zero(const uint8_t* flag, uint64_t n, uint8_t* out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint64_t grid = std::min<uint64_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(k_desc_zero, dim3((unsigned)grid), dim3(256), 0, s, flag, n, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_order_desc(const uint32_t* len, uint64_t n, void* scratch, size_t bytes,
                              uint32_t** perm, uint32_t** n_long, hipStream_t s) {
   const uint64_t arr = (n * 4 + 255) & ~(uint64_t)255;

@@ -92,6 +92,9 @@ Device::~Device() {
   for (auto& set : tev)
     for (hipEvent_t e : set)
       if (e) (void)hipEventDestroy(e);
+  if (bound_free) (void)hipEventSynchronize(bound_free);
+  (void)hipFree(bound_scratch);
+  if (bound_free) (void)hipEventDestroy(bound_free);
   if (order_free) (void)hipEventSynchronize(order_free);
   (void)hipFree(order_scratch);
   if (order_free) (void)hipEventDestroy(order_free);
@@ -1082,6 +1085,113 @@ int cir_hash_blocks_dev(cir_ctx* ctx, const void* d_arena, const uint64_t* d_off
                         const uint32_t* d_len, size_t nblk, uint8_t* d_out, void* stream) try {
   return cir_hash_blocks_dev_ht(ctx, CIR_HASH_BLAKE2B_256, d_arena, d_off, d_len, nblk, d_out,
                                 stream);
+} CIR_CATCH_BOUNDARY
+
+// Untrusted descriptors (cir_hash_blocks_dev_bounded, cir_verify_blocks_dev_
+// bounded): the bounds pass (order.hip k_desc_bound) writes checked lengths
+// and flags into scratch, the batch is hashed over the checked lengths as
+// cir_hash_blocks_dev_ht would hash it, and then the flagged blocks' digests
+// are zeroed (and failed in the compare when verifying: expected != NULL).
+// Scratch: the device's bound scratch with a context, else a stream-ordered
+// allocation freed behind the batch.  Nothing synchronises the stream.
+static int bounded_run(cir_ctx* ctx, Device* d, int ht, const uint8_t* arena,
+                       uint64_t arena_bytes, const uint64_t* off, const uint32_t* len, size_t n,
+                       uint8_t* out, uint32_t* nrange, const uint8_t* expected, uint8_t* ok,
+                       uint32_t* nbad, void* scratch, hipStream_t s) {
+  uint32_t* slen = nullptr;
+  uint8_t* flag = nullptr;
+  CIR_HIP(dev::launch_desc_bound(off, len, n, arena_bytes, scratch, nrange, &slen, &flag, s));
+  if (ctx) {
+    int rc = hash_desc_ordered(*d, arena, off, slen, n, out, s, ht);
+    if (rc) return rc;
+  } else if (ht == CIR_HASH_SHA512_256) {
+    CIR_HIP(dev::launch_sha_desc(arena, off, slen, nullptr, n, out, s));
+  } else {
+    CIR_HIP(dev::launch_general_desc(arena, off, slen, nullptr, n, out, s));
+  }
+  CIR_HIP(dev::launch_desc_zero(flag, n, out, s));
+  if (expected) CIR_HIP(dev::launch_verify(out, expected, n, ok, nbad, s, flag));
+  return CIR_OK;
+}
+
+static int hash_desc_bounded(cir_ctx* ctx, int ht, const void* d_arena, uint64_t arena_bytes,
+                             const uint64_t* d_off, const uint32_t* d_len, size_t n,
+                             uint8_t* d_out, uint32_t* d_nrange, const uint8_t* d_expected,
+                             uint8_t* d_ok, uint32_t* d_nbad, hipStream_t s) {
+  if (!valid_hash_type(ht)) return fail(CIR_EINVAL, "unknown hash type");
+  if (n && (!d_off || !d_len || !d_out)) return fail(CIR_EINVAL, "null device pointer");
+  // (d_arena may be NULL with arena_bytes == 0: every non-empty block is then
+  // out of range, and a zero-length one at offset 0 hashes as the empty input)
+  if (n && !d_arena && arena_bytes) return fail(CIR_EINVAL, "null arena with arena_bytes > 0");
+  if (reinterpret_cast<uintptr_t>(d_out) & 15u)
+    return fail(CIR_EINVAL, "digest arrays must be 16-byte aligned");
+  if (n > (size_t)INT32_MAX) return fail(CIR_EINVAL, "more than 2^31-1 descriptors");
+  Device* d = nullptr;
+  if (ctx) {
+    d = stream_device(ctx, s);
+    if (!d) return fail(CIR_EINVAL, "stream device is not part of the context");
+  }
+  if (d_nbad) CIR_HIP(hipMemsetAsync(d_nbad, 0, 4, s));
+  if (n == 0) {
+    if (d_nrange) CIR_HIP(hipMemsetAsync(d_nrange, 0, 4, s));
+    return CIR_OK;
+  }
+  const uint8_t* arena = static_cast<const uint8_t*>(d_arena);
+  const size_t need = dev::bound_scratch_bytes(n);
+  if (!d) {
+    void* scratch = nullptr;
+    CIR_HIP(hipMallocAsync(&scratch, need, s));
+    const int rc = bounded_run(ctx, d, ht, arena, arena_bytes, d_off, d_len, n, d_out, d_nrange,
+                               d_expected, d_ok, d_nbad, scratch, s);
+    const hipError_t e = hipFreeAsync(scratch, s);
+    if (rc) return rc;
+    CIR_HIP(e);
+    return CIR_OK;
+  }
+  std::lock_guard<std::mutex> lk(d->bound_mu);
+  DeviceGuard guard;
+  CIR_HIP(hipSetDevice(d->id));
+  if (!d->bound_free) CIR_HIP(hipEventCreateWithFlags(&d->bound_free, hipEventDisableTiming));
+  if (need > d->bound_cap) {
+    // grows with the batch: a larger batch than any before waits for the
+    // previous user of the scratch
+    CIR_HIP(hipEventSynchronize(d->bound_free));
+    (void)hipFree(d->bound_scratch);
+    d->bound_scratch = nullptr;
+    d->bound_cap = 0;
+    CIR_HIP(hipMalloc(&d->bound_scratch, need));
+    d->bound_cap = need;
+  }
+  CIR_HIP(hipStreamWaitEvent(s, d->bound_free, 0));
+  const int rc = bounded_run(ctx, d, ht, arena, arena_bytes, d_off, d_len, n, d_out, d_nrange,
+                             d_expected, d_ok, d_nbad, d->bound_scratch, s);
+  // recorded on every path: whatever of the batch was queued is ordered
+  // before the scratch's next user
+  const hipError_t e = hipEventRecord(d->bound_free, s);
+  if (rc) return rc;
+  CIR_HIP(e);
+  return CIR_OK;
+}
+
+int cir_hash_blocks_dev_bounded(cir_ctx* ctx, int hash_type, const void* d_arena,
+                                uint64_t arena_bytes, const uint64_t* d_off, const uint32_t* d_len,
+                                size_t nblk, uint8_t* d_out, uint32_t* d_nrange,
+                                void* stream) try {
+  return hash_desc_bounded(ctx, hash_type, d_arena, arena_bytes, d_off, d_len, nblk, d_out,
+                           d_nrange, nullptr, nullptr, nullptr, (hipStream_t)stream);
+} CIR_CATCH_BOUNDARY
+
+int cir_verify_blocks_dev_bounded(cir_ctx* ctx, int hash_type, const void* d_arena,
+                                  uint64_t arena_bytes, const uint64_t* d_off,
+                                  const uint32_t* d_len, size_t nblk, const uint8_t* d_expected,
+                                  uint8_t* d_digests, uint8_t* d_ok, uint32_t* d_nbad,
+                                  void* stream) try {
+  if (nblk && (!d_expected || !d_digests)) return fail(CIR_EINVAL, "null device pointer");
+  if ((reinterpret_cast<uintptr_t>(d_expected) | reinterpret_cast<uintptr_t>(d_digests)) & 15u)
+    return fail(CIR_EINVAL, "digest arrays must be 16-byte aligned");
+  // (nblk == 0: *d_nbad = 0 and nothing else happens)
+  return hash_desc_bounded(ctx, hash_type, d_arena, arena_bytes, d_off, d_len, nblk, d_digests,
+                           nullptr, d_expected, d_ok, d_nbad, (hipStream_t)stream);
 } CIR_CATCH_BOUNDARY
 
 int cir_hash_blocks_ht(cir_ctx* ctx, int hash_type, const uint8_t* h_arena, const uint64_t* off,

@@ -149,6 +149,14 @@ struct Device {
   void* order_scratch = nullptr;
   size_t order_cap = 0;
   hipEvent_t order_free = nullptr;
+  // scratch of the bounds pass of the *_dev_bounded entry points (checked
+  // lengths and flags, order.hip launch_desc_bound), kept across calls like
+  // the ordering scratch; users on different streams are ordered through
+  // `bound_free` (created on first use).  Taken before order_mu.
+  std::mutex bound_mu;
+  void* bound_scratch = nullptr;
+  size_t bound_cap = 0;
+  hipEvent_t bound_free = nullptr;
   // An ordered batch runs its quad part on `qstream` (a high-priority
   // stream: a hardware queue of its own) and its lane part on the caller's
   // stream, forked and joined with events (runtime.cpp create_part_streams).

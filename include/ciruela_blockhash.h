@@ -12,8 +12,14 @@
  * Conventions
  *   - return 0 (CIR_OK) on success, a negative CIR_E* code on failure; the
  *     detail of the last failure is in cir_last_error().  No call aborts the
- *     process (the reference panics only on impossible states, e.g.
- *     src/block_id.rs:38,41 "length is ok").
+ *     process on bad input it can check (the reference panics only on
+ *     impossible states, e.g. src/block_id.rs:38,41 "length is ok").  The
+ *     caller's own buffers are trusted, as a slice is in the reference: the
+ *     descriptor batches cir_hash_blocks_dev[_ht] and cir_verify_blocks_dev
+ *     read arena + off[b] .. + len[b] as given (an out-of-range descriptor is
+ *     a GPU memory fault), so descriptors derived from untrusted data go
+ *     through the *_dev_bounded entry points, which check every one against
+ *     the arena's size on the device.
  *   - digests are 32 raw bytes (BlockHash([u8; 32]), src/block_id.rs:19),
  *     printed as lowercase hex (src/hexlify.rs:9-13).
  *   - `stream` arguments are hipStream_t passed as void* (NULL = the null
@@ -158,6 +164,22 @@ int cir_hash_chunks_dev(cir_ctx* ctx, const void* d_data, uint64_t nbytes, uint6
 int cir_hash_blocks_dev(cir_ctx* ctx, const void* d_arena, const uint64_t* d_off,
                         const uint32_t* d_len, size_t nblk, uint8_t* d_out, void* stream);
 
+/* cir_hash_blocks_dev_ht for descriptors the caller cannot vouch for (the
+ * daemon's received blocks, src/daemon/tracking/fetch_blocks.rs:77,91-103):
+ * the arena is [d_arena, d_arena + arena_bytes), and block b is out of range
+ * when d_off[b] + d_len[b] wraps around 2^64 or passes arena_bytes.  An
+ * out-of-range block is not read (no kernel touches memory outside the
+ * arena); its digest is 32 zero bytes and *d_nrange (device u32, may be
+ * NULL) = the number of such blocks.  The other blocks' digests are exactly
+ * cir_hash_blocks_dev_ht's.  Asynchronous on `stream` like the other *_dev
+ * calls: the caller reads *d_nrange after its own synchronisation and treats
+ * a non-zero count as CIR_EINVAL for those blocks.  Costs one extra pass
+ * over the descriptors (12 B read, 5 B written per block) and, with a
+ * context, a device scratch of ~5 B per block kept for the next call. */
+int cir_hash_blocks_dev_bounded(cir_ctx* ctx, int hash_type, const void* d_arena,
+                                uint64_t arena_bytes, const uint64_t* d_off, const uint32_t* d_len,
+                                size_t nblk, uint8_t* d_out, uint32_t* d_nrange, void* stream);
+
 /* Host-memory batch (same meaning as cir_hash_blocks_dev, host pointers);
  * staged through pinned buffers, split across the context's devices. */
 int cir_hash_blocks(cir_ctx* ctx, const uint8_t* h_arena, const uint64_t* off,
@@ -204,6 +226,18 @@ int cir_hash_memory_ht(cir_ctx* ctx, int hash_type, const uint8_t* data, uint64_
 int cir_verify_blocks_dev(cir_ctx* ctx, int hash_type, const void* d_arena, const uint64_t* d_off,
                           const uint32_t* d_len, size_t nblk, const uint8_t* d_expected,
                           uint8_t* d_digests, uint8_t* d_ok, uint32_t* d_nbad, void* stream);
+
+/* cir_verify_blocks_dev over untrusted descriptors, as
+ * cir_hash_blocks_dev_bounded checks them: an out-of-range block (d_off[b] +
+ * d_len[b] wraps or passes arena_bytes) is never read and counts as a
+ * mismatch -- d_ok[b] = 0, included in *d_nbad -- so the caller re-fetches
+ * it as it would a corrupted block (fetch_blocks.rs:91-103); its
+ * d_digests entry is 32 zero bytes. */
+int cir_verify_blocks_dev_bounded(cir_ctx* ctx, int hash_type, const void* d_arena,
+                                  uint64_t arena_bytes, const uint64_t* d_off,
+                                  const uint32_t* d_len, size_t nblk, const uint8_t* d_expected,
+                                  uint8_t* d_digests, uint8_t* d_ok, uint32_t* d_nbad,
+                                  void* stream);
 
 /* Host-memory batch of the same check; ok_out (nblk bytes) may be NULL. */
 int cir_verify_blocks(cir_ctx* ctx, int hash_type, const uint8_t* h_arena, const uint64_t* off,

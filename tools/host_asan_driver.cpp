@@ -215,6 +215,39 @@ static void device_paths(cir_ctx* ctx, int ht) {
   CHECK(hipMemcpy(&nbad, d_nbad, 4, hipMemcpyDeviceToHost) == hipSuccess);
   CHECK(hipMemcpy(ok.data(), d_ok, nblk, hipMemcpyDeviceToHost) == hipSuccess);
   CHECK(nbad == 1 && ok[nblk - 1] == 0 && (nblk == 1 || ok[0] == 1));
+  // the bounded entry points take the descriptors unchecked: two of them
+  // leave the arena (past its end, and wrapping around 2^64) and must come
+  // back flagged, never read
+  want[32 * (nblk - 1)] ^= 2;
+  const uint64_t b1 = rng() % nblk, b2 = (b1 + 1) % nblk;
+  off[b1] = nbytes + 1 - len[b1];  // ends one byte past the arena
+  off[b2] = ~0ull - 7;
+  len[b2] = 64;
+  CHECK(hipMemcpy(d_off, off.data(), 8 * nblk, hipMemcpyHostToDevice) == hipSuccess);
+  CHECK(hipMemcpy(d_len, len.data(), 4 * nblk, hipMemcpyHostToDevice) == hipSuccess);
+  CHECK(cir_hash_blocks_dev_bounded(ctx, ht, d_data, nbytes, d_off, d_len, nblk, d_out, d_nbad,
+                                    st) == 0);
+  CHECK(hipStreamSynchronize(st) == hipSuccess);
+  CHECK(hipMemcpy(got.data(), d_out, got.size(), hipMemcpyDeviceToHost) == hipSuccess);
+  CHECK(hipMemcpy(&nbad, d_nbad, 4, hipMemcpyDeviceToHost) == hipSuccess);
+  const uint32_t nflag = b1 == b2 ? 1 : 2;
+  CHECK(nbad == nflag);
+  for (uint64_t b = 0; b < nblk; ++b) {
+    if (b == b1 || b == b2) {
+      for (int k = 0; k < 32; ++k) CHECK(got[32 * b + k] == 0);
+      std::fill(want.begin() + 32 * b, want.begin() + 32 * b + 32, 0);
+    } else {
+      CHECK(memcmp(&got[32 * b], &want[32 * b], 32) == 0);
+    }
+  }
+  CHECK(hipMemcpy(d_exp, want.data(), want.size(), hipMemcpyHostToDevice) == hipSuccess);
+  CHECK(cir_verify_blocks_dev_bounded(ctx, ht, d_data, nbytes, d_off, d_len, nblk, d_exp, d_dig,
+                                      d_ok, d_nbad, st) == 0);
+  CHECK(hipStreamSynchronize(st) == hipSuccess);
+  CHECK(hipMemcpy(&nbad, d_nbad, 4, hipMemcpyDeviceToHost) == hipSuccess);
+  CHECK(hipMemcpy(ok.data(), d_ok, nblk, hipMemcpyDeviceToHost) == hipSuccess);
+  CHECK(nbad == nflag);  // a zero expected digest does not make them match
+  for (uint64_t b = 0; b < nblk; ++b) CHECK(ok[b] == ((b == b1 || b == b2) ? 0 : 1));
   for (void* p : {(void*)d_data, (void*)d_out, (void*)d_off, (void*)d_len, (void*)d_exp, (void*)d_dig,
                   (void*)d_ok, (void*)d_nbad})
     (void)hipFree(p);
