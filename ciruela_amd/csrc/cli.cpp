@@ -54,25 +54,48 @@ static int die(int rc, const char* what) {
 
 // Bytes of the regular files under path, counted only until they reach cap.
 // The top-level argument is followed as the scan and the hash path follow it
-// (opendir / open): a symlinked SRC or FILE counts its target; entries inside
-// directories are not followed (lstat), as walk() does.  A top-level argument
-// that is neither a regular file nor a directory (a pipe, /dev/stdin) has no
-// size to count and gets the default staging (returns cap).
-static uint64_t tree_bytes(const std::string& path, uint64_t cap, uint64_t acc = 0,
-                           bool top = true) {
-  struct stat st;
-  if (acc >= cap) return acc;
-  if ((top ? stat(path.c_str(), &st) : lstat(path.c_str(), &st)) != 0) return top ? cap : acc;
-  if (S_ISREG(st.st_mode)) return acc + (uint64_t)st.st_size;
-  if (!S_ISDIR(st.st_mode)) return top ? cap : acc;
-  DIR* d = opendir(path.c_str());
-  if (!d) return acc;
+// (open): a symlinked SRC or FILE counts its target; entries inside
+// directories are not followed (fstatat AT_SYMLINK_NOFOLLOW), as the scan's
+// walk does, and each directory is read through its own fd opened from its
+// parent's (openat), so a tree nested past PATH_MAX is counted too.  A
+// top-level argument that is neither a regular file nor a directory (a pipe,
+// /dev/stdin) has no size to count and gets the default staging (returns cap).
+static uint64_t dir_bytes(int dfd, uint64_t cap, uint64_t acc) {
+  const int lfd = fcntl(dfd, F_DUPFD_CLOEXEC, 0);
+  DIR* d = lfd >= 0 ? fdopendir(lfd) : nullptr;
+  if (!d) {
+    if (lfd >= 0) close(lfd);
+    return acc;
+  }
   while (struct dirent* e = readdir(d)) {
     if (!strcmp(e->d_name, ".") || !strcmp(e->d_name, "..")) continue;
-    acc = tree_bytes(path + "/" + e->d_name, cap, acc, false);
+    struct stat st;
+    if (fstatat(dfd, e->d_name, &st, AT_SYMLINK_NOFOLLOW) != 0) continue;
+    if (S_ISREG(st.st_mode)) {
+      acc += (uint64_t)st.st_size;
+    } else if (S_ISDIR(st.st_mode)) {
+      const int cfd = openat(dfd, e->d_name, O_RDONLY | O_DIRECTORY | O_NOFOLLOW | O_CLOEXEC);
+      if (cfd >= 0) {
+        acc = dir_bytes(cfd, cap, acc);
+        close(cfd);
+      }
+    }
     if (acc >= cap) break;
   }
   closedir(d);
+  return acc;
+}
+
+static uint64_t tree_bytes(const std::string& path, uint64_t cap, uint64_t acc) {
+  struct stat st;
+  if (acc >= cap) return acc;
+  if (stat(path.c_str(), &st) != 0) return cap;
+  if (S_ISREG(st.st_mode)) return acc + (uint64_t)st.st_size;
+  if (!S_ISDIR(st.st_mode)) return cap;
+  const int fd = open(path.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+  if (fd < 0) return acc;
+  acc = dir_bytes(fd, cap, acc);
+  close(fd);
   return acc;
 }
 
@@ -211,7 +234,9 @@ int main(int argc, char** argv) {
   // slot (256 MiB) is one batch on one GPU -- instead of every GPU of the
   // node (each costs its device context, streams and 834 MiB of pinned
   // staging at start-up, include/ciruela_blockhash.h)
-  const uint32_t ndev = cir_devices_for_bytes(total, staging, 32);
+  // (an empty input -- empty files, an empty tree -- is measured, not
+  // unknown: one device, not cir_devices_for_bytes' "0 = every device")
+  const uint32_t ndev = cir_devices_for_bytes(std::max<uint64_t>(total, 1), staging, 32);
   const auto t_init = std::chrono::steady_clock::now();
   // and a small input is one short job: one stream and one slot per device
   // (CIR_INIT_ONE_SHOT; the other streams' hardware queues were ~25 ms of

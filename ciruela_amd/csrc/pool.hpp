@@ -52,16 +52,25 @@ class WorkerPool {
     job.fn = &fn;
     {
       std::lock_guard<std::mutex> lk(mu_);
-      for (unsigned i = 0; i + 1 < n; ++i) q_.push_back(&job);
-      job.pending = n - 1;
+      unsigned queued = 0;
+      try {
+        for (; queued + 1 < n; ++queued) q_.push_back(&job);
+      } catch (...) {
+        // out of memory part-way: take this job's tickets back (the last
+        // `queued` entries: the lock is held) and run it on this thread only
+        // -- a ticket left queued would point at `job` after it is gone
+        for (; queued > 0; --queued) q_.pop_back();
+      }
+      job.pending = queued;
       // a worker for every ticket queued or running, concurrent callers
       // included (several devices' readers at once)
       const size_t want = std::min<size_t>(busy_ + q_.size(), kMaxWorkers);
       try {
         while (th_.size() < want) th_.emplace_back([this] { loop(); });
-      } catch (const std::system_error&) {
-        // (no thread for now: the tickets wait for a free worker or are
-        // dropped once the caller's own run has done the work)
+      } catch (...) {
+        // (no thread for now -- system_error, or bad_alloc for its state or
+        // the vector: the tickets wait for a free worker or are dropped once
+        // the caller's own run has done the work)
       }
     }
     cv_.notify_all();

@@ -193,8 +193,11 @@ void fan_out(size_t n, const std::function<void(size_t)>& fn) {
   for (size_t i = 0; i < n; ++i) {
     try {
       th.emplace_back(one, i);
-    } catch (const std::system_error&) {
-      here.push_back(i);  // no thread: run it on this one below
+    } catch (...) {
+      // no thread (system_error, or bad_alloc for its state): run it on this
+      // one below.  (`here` was reserved: the push cannot throw, so no
+      // exception leaves while `th` holds joinable threads.)
+      here.push_back(i);
     }
   }
   for (size_t i : here) one(i);

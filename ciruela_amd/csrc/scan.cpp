@@ -16,6 +16,7 @@
 #include <stdio.h>
 #include <errno.h>
 #include <fcntl.h>
+#include <limits.h>
 #include <string.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -53,6 +54,41 @@ struct PlanItem {
   std::string target;  // kLink
 };
 
+// open(2) for a path of any length.  Below PATH_MAX the path opens as it
+// is; a longer one is opened piecewise -- each piece shorter than PATH_MAX
+// and ending at a '/' -- relative to the directory the previous piece opened
+// (openat), so the files of a tree nested past PATH_MAX still open.
+static int open_long(const std::string& path, int flags) {
+  flags |= O_CLOEXEC;
+  if (path.size() < PATH_MAX) return ::open(path.c_str(), flags);
+  int dfd = AT_FDCWD;
+  size_t pos = 0;
+  auto drop = [&dfd] {
+    if (dfd != AT_FDCWD) {
+      const int e = errno;
+      ::close(dfd);
+      errno = e;
+    }
+  };
+  while (path.size() - pos >= PATH_MAX) {
+    const size_t cut = path.rfind('/', pos + PATH_MAX - 2);
+    if (cut == std::string::npos || cut < pos) {  // one component longer than PATH_MAX
+      drop();
+      errno = ENAMETOOLONG;
+      return -1;
+    }
+    const std::string piece = cut > pos ? path.substr(pos, cut - pos) : pos == 0 ? "/" : ".";
+    const int nfd = ::openat(dfd, piece.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+    drop();
+    if (nfd < 0) return -1;
+    dfd = nfd;
+    pos = cut + 1;
+  }
+  const int fd = ::openat(dfd, path.c_str() + pos, flags);
+  drop();
+  return fd;
+}
+
 // The tree walk.  Directories are read in parallel -- each one's entries
 // listed, sorted and lstat'ed by whichever walker thread takes it, its
 // subdirectories queued for the others (a tree of many small files is
@@ -61,8 +97,18 @@ struct PlanItem {
 // calling thread in the serial walk's order: a directory's line, its files
 // and symlinks in name order, then its subdirectories in name order, depth
 // first.  A failure is reported as the serial walk would meet it first: a
-// directory's own error (opendir, an lstat, a readlink) before anything
-// below it.
+// directory's own error (opening or listing it, an lstat, a readlink) before
+// anything below it.
+//
+// Every directory is opened relative to its parent's fd (openat with
+// O_NOFOLLOW: the entry lstat'ed as a directory is the one read) and listed,
+// lstat'ed and read-linked through its own fd (fdopendir, fstatat
+// AT_SYMLINK_NOFOLLOW, readlinkat), as dir-signature 0.2.9 walks with openat
+// (Cargo.lock:323): no call takes the full path, so a tree nested past
+// PATH_MAX indexes like any other.  A directory's fd stays open until it has
+// been listed and every subdirectory has opened its own from it (a count of
+// holders); subdirectories are taken last-queued first, so the fds open at
+// once stay near the walkers' depth, not the tree's width.
 struct DirNode {
   struct Ent {
     std::string name;
@@ -70,39 +116,80 @@ struct DirNode {
     uint64_t size = 0;
     std::string target;  // symlinks
   };
-  std::string real, vpath;
+  std::string real, vpath, name;  // name: the entry in the parent
+  DirNode* parent = nullptr;
+  int fd = -1;
+  std::atomic<size_t> holders{1};  // itself while it is read, then each unopened subdir
   std::vector<Ent> ents;  // files and symlinks, name order
   std::vector<std::unique_ptr<DirNode>> subdirs;  // name order
   int rc = CIR_OK;
   std::string err;  // the first failure met in this directory
 };
 
+static void release_fd(DirNode& n) {
+  if (n.holders.fetch_sub(1) == 1 && n.fd >= 0) {
+    ::close(n.fd);
+    n.fd = -1;
+  }
+}
+
 static void read_dir(DirNode& n) {
-  DIR* d = opendir(n.real.c_str());
-  if (!d) {
+  // this directory's fd: the root by its path, the rest relative to the
+  // parent's (which stays open for it), never through a symlink
+  n.fd = n.parent
+             ? ::openat(n.parent->fd, n.name.c_str(),
+                        O_RDONLY | O_DIRECTORY | O_NOFOLLOW | O_CLOEXEC)
+             : open_long(n.real, O_RDONLY | O_DIRECTORY);
+  const int open_errno = errno;
+  if (n.parent) release_fd(*n.parent);
+  if (n.fd < 0) {
     n.rc = CIR_EIO;
-    n.err = "error indexing dir " + n.real + ": " + strerror(errno);
+    n.err = "error indexing dir " + n.real + ": " + strerror(open_errno);
+    return;
+  }
+  // (fdopendir owns the fd it is given: a duplicate, so n.fd stays ours)
+  const int lfd = ::fcntl(n.fd, F_DUPFD_CLOEXEC, 0);
+  DIR* d = lfd >= 0 ? ::fdopendir(lfd) : nullptr;
+  if (!d) {
+    const int e = errno;
+    if (lfd >= 0) ::close(lfd);
+    n.rc = CIR_EIO;
+    n.err = "error indexing dir " + n.real + ": " + strerror(e);
     return;
   }
   std::vector<std::string> names;
-  while (struct dirent* de = readdir(d)) {
+  for (;;) {
+    errno = 0;
+    struct dirent* de = ::readdir(d);
+    if (!de) {
+      // NULL is the end of the directory only when errno is untouched
+      if (errno != 0) {
+        const int e = errno;
+        ::closedir(d);
+        n.rc = CIR_EIO;
+        n.err = "error reading dir " + n.real + ": " + strerror(e);
+        return;
+      }
+      break;
+    }
     if (!strcmp(de->d_name, ".") || !strcmp(de->d_name, "..")) continue;
     names.emplace_back(de->d_name);
   }
-  closedir(d);
+  ::closedir(d);
   std::sort(names.begin(), names.end());
   for (std::string& nm : names) {
-    const std::string p = n.real + "/" + nm;
     struct stat st;
-    if (lstat(p.c_str(), &st) != 0) {
+    if (::fstatat(n.fd, nm.c_str(), &st, AT_SYMLINK_NOFOLLOW) != 0) {
       n.rc = CIR_EIO;
-      n.err = "error indexing dir " + p + ": " + strerror(errno);
+      n.err = "error indexing dir " + n.real + "/" + nm + ": " + strerror(errno);
       return;
     }
     if (S_ISDIR(st.st_mode)) {
       auto c = std::make_unique<DirNode>();
-      c->real = p;
+      c->real = n.real + "/" + nm;
       c->vpath = n.vpath == "/" ? "/" + nm : n.vpath + "/" + nm;
+      c->name = std::move(nm);
+      c->parent = &n;
       n.subdirs.push_back(std::move(c));
     } else if (S_ISREG(st.st_mode)) {
       DirNode::Ent e;
@@ -112,10 +199,10 @@ static void read_dir(DirNode& n) {
       n.ents.push_back(std::move(e));
     } else if (S_ISLNK(st.st_mode)) {
       std::string tgt(4096, '\0');
-      const ssize_t r = readlink(p.c_str(), &tgt[0], tgt.size());
+      const ssize_t r = ::readlinkat(n.fd, nm.c_str(), &tgt[0], tgt.size());
       if (r < 0) {
         n.rc = CIR_EIO;
-        n.err = "error reading link " + p + ": " + strerror(errno);
+        n.err = "error reading link " + n.real + "/" + nm + ": " + strerror(errno);
         return;
       }
       tgt.resize((size_t)r);
@@ -159,6 +246,12 @@ static int emit_plan(DirNode& n, std::vector<PlanItem>& plan, std::vector<ScanFi
   return CIR_OK;
 }
 
+static void close_all(DirNode& n) {
+  if (n.fd >= 0) ::close(n.fd);
+  n.fd = -1;
+  for (auto& c : n.subdirs) close_all(*c);
+}
+
 static int walk(const std::string& real, const std::string& vpath, unsigned threads,
                 std::vector<PlanItem>& plan, std::vector<ScanFile>& files) {
   DirNode root;
@@ -166,15 +259,15 @@ static int walk(const std::string& real, const std::string& vpath, unsigned thre
   root.vpath = vpath;
   std::mutex mu;
   std::condition_variable cv;
-  std::deque<DirNode*> queue{&root};
+  std::vector<DirNode*> stack{&root};  // last queued first (see above)
   size_t busy = 0;
   parallel_run(std::max(1u, threads), [&] {
     std::unique_lock<std::mutex> lk(mu);
     for (;;) {
-      cv.wait(lk, [&] { return !queue.empty() || busy == 0; });
-      if (queue.empty()) return;  // nothing queued, nobody reading: done
-      DirNode* n = queue.front();
-      queue.pop_front();
+      cv.wait(lk, [&] { return !stack.empty() || busy == 0; });
+      if (stack.empty()) return;  // nothing queued, nobody reading: done
+      DirNode* n = stack.back();
+      stack.pop_back();
       ++busy;
       lk.unlock();
       try {
@@ -184,19 +277,28 @@ static int walk(const std::string& real, const std::string& vpath, unsigned thre
         n->err = "walking " + n->real + ": out of memory";
         n->subdirs.clear();
       }
+      if (n->rc != CIR_OK) n->subdirs.clear();  // none of them will be read
+      // each subdirectory holds this fd until it has opened its own; the
+      // read itself lets go of it now
+      n->holders.fetch_add(n->subdirs.size());
+      release_fd(*n);
       lk.lock();
       --busy;
       if (n->rc == CIR_OK) {
         try {
-          for (auto& c : n->subdirs) queue.push_back(c.get());
+          // pushed in reverse name order: the first subdirectory is read first
+          for (auto it = n->subdirs.rbegin(); it != n->subdirs.rend(); ++it)
+            stack.push_back(it->get());
         } catch (...) {  // (the others must still be woken below)
           n->rc = CIR_ENOMEM;
           n->err = "walking " + n->real + ": out of memory";
+          // the subdirectories not queued still hold this fd: close_all
         }
       }
       cv.notify_all();
     }
   });
+  close_all(root);  // (only an out-of-memory walk leaves an fd open)
   return emit_plan(root, plan, files);
 }
 
@@ -232,7 +334,7 @@ static int run_reads(const std::vector<ReadJob>& jobs, const std::vector<ScanFil
       if (i >= jobs.size() || rc.load()) return;
       const ReadJob& j = jobs[i];
       const std::string& path = files[j.file].real;
-      const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+      const int fd = open_long(path, O_RDONLY);
       bool ok = fd >= 0;
       uint64_t got = 0;
       while (ok && got < j.len) {
@@ -560,13 +662,15 @@ struct FooterChain {
     return ms;
   }
 
+  // (caller holds d.chain_mu.)  A one-shot context's device has the chain
+  // state and events from cir_init but no chain stream: each piece missing
+  // is created here, and only those.
   int start() {
-    if (!d.chain) {
-      CIR_HIP(hipStreamCreateWithFlags(&d.chain, hipStreamNonBlocking));
-      CIR_HIP(hipMalloc(&d.chain_state, 16 * 8));
-      for (int b = 0; b < 2; ++b) CIR_HIP(hipEventCreateWithFlags(&d.chain_done[b],
-                                                                 hipEventDisableTiming));
-    }
+    if (!d.chain) CIR_HIP(hipStreamCreateWithFlags(&d.chain, hipStreamNonBlocking));
+    if (!d.chain_state) CIR_HIP(hipMalloc(&d.chain_state, 16 * 8));
+    for (int b = 0; b < 2; ++b)
+      if (!d.chain_done[b])
+        CIR_HIP(hipEventCreateWithFlags(&d.chain_done[b], hipEventDisableTiming));
     CIR_HIP(hipMemsetAsync(d.chain_state, 0, 16 * 8, d.chain));
     fed = 0;
     return CIR_OK;

@@ -54,6 +54,12 @@ class VerifyQueue {
                                    const uint32_t* len, size_t n, uint8_t* out, std::string* err)>;
   static constexpr uint64_t kMaxBytes = 256ull << 20;  // two batches of 4096 x 32 KiB
   static constexpr uint64_t kMaxResults = 1ull << 20;
+  // a batch's arena: half the byte bound (a batch forms while the previous
+  // one is verified), at most one full batch of 32 KiB blocks -- the bound
+  // caps what is admitted, not what one batch allocates, so a large bound
+  // costs nothing up front; only a block larger than this gets an arena of
+  // its own size
+  static constexpr uint64_t kArenaMax = 4096ull * 32768;
 
   explicit VerifyQueue(HashFn hash) : hash_(std::move(hash)) {
     worker_ = std::thread([this] { run(); });
@@ -104,12 +110,12 @@ class VerifyQueue {
     if (!b) {
       auto nb = std::make_unique<Batch>();
       nb->ht = ht;
-      // one batch's arena: half the byte bound, so a batch can form while
-      // the previous one is verified; a spare arena of a verified batch is
-      // reused (its pages are already faulted in)
-      if (!arena_for(*nb, std::max<uint64_t>(n, std::max<uint64_t>(1, max_bytes_ / 2)))) {
-        *err = "verify batch arena of " + std::to_string(std::max<uint64_t>(n, max_bytes_ / 2)) +
-               " bytes";
+      // one batch's arena (arena_bytes(); a spare arena of a verified batch
+      // is reused: its pages are already faulted in), or -- when that much
+      // cannot be allocated -- one just for this block
+      if (!arena_for(*nb, std::max<uint64_t>(n, arena_bytes())) &&
+          (n >= arena_bytes() || !arena_for(*nb, std::max<uint64_t>(n, 1)))) {
+        *err = "verify batch arena of " + std::to_string(std::max<uint64_t>(n, 1)) + " bytes";
         return CIR_ENOMEM;
       }
       nb->first = std::chrono::steady_clock::now();
@@ -243,6 +249,11 @@ class VerifyQueue {
     return r;
   }
 
+  // the standard arena of a batch (see kArenaMax); caller holds mu_
+  uint64_t arena_bytes() const {
+    return std::max<uint64_t>(1, std::min<uint64_t>(max_bytes_ / 2, kArenaMax));
+  }
+
   // b gets an arena of at least `bytes`: a spare one when one is big enough;
   // false if it cannot be allocated (caller holds mu_)
   bool arena_for(Batch& b, uint64_t bytes) {
@@ -308,7 +319,7 @@ class VerifyQueue {
       evict();
       // keep the arena for a later batch (at most two spares, within the
       // byte bound's two batches); the rest is freed outside the lock
-      if (spare_.size() < 2 && bp->cap <= std::max<uint64_t>(1, max_bytes_ / 2))
+      if (spare_.size() < 2 && bp->cap <= arena_bytes())
         spare_.emplace_back(std::move(bp->arena), bp->cap);
       room_cv_.notify_all();
       done_cv_.notify_all();

@@ -258,8 +258,9 @@ int cir_verify_blocks(cir_ctx* ctx, int hash_type, const uint8_t* h_arena, const
  * (microseconds) and the batch cap.
  *
  * Bounds (cir_verify_limits; 0 = the default):
- *   max_bytes    block bytes accepted and not yet verified (default 256 MiB;
- *                a batch's arena holds at most half of it).  A submit that
+ *   max_bytes    block bytes accepted and not yet verified (default 256 MiB).
+ *                It bounds admission only: a batch's arena holds min(half of
+ *                it, 128 MiB), so a large bound allocates nothing up front.  A submit that
  *                would pass it waits until the worker has verified enough,
  *                or with flags = CIR_VERIFY_NONBLOCK returns CIR_EAGAIN (the
  *                block is not taken: retry later or elsewhere).  A block

@@ -75,29 +75,63 @@ def emit(hash_name, block_size, dirs, keep_empty=False):
     return header + body + footer
 
 
+_DIR_FLAGS = os.O_RDONLY | os.O_DIRECTORY | getattr(os, "O_CLOEXEC", 0)
+
+
+def open_rel(root, parts, flags=os.O_RDONLY):
+    """fd of root/parts[0]/.../parts[-1] opened one component at a time
+    relative to its parent's fd (openat), so a path of any length opens;
+    directories below the root are not followed through symlinks."""
+    fd = os.open(root, _DIR_FLAGS)
+    try:
+        for c in parts[:-1]:
+            nfd = os.open(c, _DIR_FLAGS | os.O_NOFOLLOW, dir_fd=fd)
+            os.close(fd)
+            fd = nfd
+        return os.open(parts[-1], flags | getattr(os, "O_CLOEXEC", 0), dir_fd=fd)
+    finally:
+        os.close(fd)
+
+
 def walk(root):
     """The tree at `root` mounted at '/': [(vpath, [entries])] in emission
-    order, file entries ('f', name, exe, size, real_path) not yet hashed."""
+    order, file entries ('f', name, exe, size, real_path, parts) not yet
+    hashed (parts: the path's components below root, for open_rel).
+
+    Every directory is listed, lstat'ed and read-linked through its own fd
+    (os.listdir(fd), os.stat(.., dir_fd=, follow_symlinks=False),
+    os.readlink(.., dir_fd=)), each opened relative to its parent's, as
+    dir-signature 0.2.9 walks with openat (Cargo.lock:323): a tree whose
+    paths pass PATH_MAX indexes like any other."""
     dirs = []
 
-    def rec(real, vpath):
-        names = sorted(os.listdir(os.fsencode(real)))
+    def rec(fd, parts, vpath):
+        # os.listdir(fd) gives str names (surrogate-escaped): back to raw bytes
+        names = sorted(os.fsencode(n) for n in os.listdir(fd))
         entries, subdirs = [], []
+        base = os.path.join(os.fsencode(root), *parts) if parts else os.fsencode(root)
         for n in names:
-            p = os.path.join(os.fsencode(real), n)
-            st = os.lstat(p)
+            st = os.stat(n, dir_fd=fd, follow_symlinks=False)
             if stat.S_ISDIR(st.st_mode):
                 subdirs.append(n)
             elif stat.S_ISREG(st.st_mode):
-                entries.append(("f", n, bool(st.st_mode & 0o111), st.st_size, p))
+                entries.append(("f", n, bool(st.st_mode & 0o111), st.st_size,
+                                os.path.join(base, n), parts + (n,)))
             elif stat.S_ISLNK(st.st_mode):
-                entries.append(("s", n, os.readlink(p)))
+                entries.append(("s", n, os.readlink(n, dir_fd=fd)))
         dirs.append((vpath, entries))
         for n in subdirs:
-            rec(os.path.join(os.fsencode(real), n),
-                (b"/" + n) if vpath == b"/" else vpath + b"/" + n)
+            cfd = os.open(n, _DIR_FLAGS | os.O_NOFOLLOW, dir_fd=fd)
+            try:
+                rec(cfd, parts + (n,), (b"/" + n) if vpath == b"/" else vpath + b"/" + n)
+            finally:
+                os.close(cfd)
 
-    rec(root, b"/")
+    top = os.open(root, _DIR_FLAGS)
+    try:
+        rec(top, (), b"/")
+    finally:
+        os.close(top)
     return dirs
 
 
@@ -117,7 +151,7 @@ def scan(root, block_size=32768, hash_name="blake2b/256", block_hasher=None, fil
         hasher = block_hasher or (lambda data, bs: block_hashes(data, bs, hash_name))
         digests = []
         for e in files:
-            with open(e[4], "rb") as f:
+            with os.fdopen(open_rel(root, e[5]), "rb") as f:
                 data = f.read()
             assert len(data) == e[3], "file changed during the scan"
             digests.append(hasher(data, block_size))

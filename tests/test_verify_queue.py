@@ -9,8 +9,9 @@ ASan + UBSan (tools/verify_queue_stress.cpp):
     bound is taken alone; forget of a pending ticket (releasing its waiter),
     of a finished one and of an unknown one; expiry keeps the newest
     max_results outcomes; a failed batch reports its code to every ticket;
-    two hash types never share a batch; an arena that cannot be allocated
-    is CIR_ENOMEM;
+    two hash types never share a batch; a bound larger than memory still
+    verifies (arenas stay at most 128 MiB), a block whose own arena cannot
+    be allocated is CIR_ENOMEM;
   * random traffic from 2-5 threads, blocking and not, with forgets and
     polls: every outcome right, the peak within the bound, nothing held at
     the end, and a queue destroyed with work queued drains it.
