@@ -466,6 +466,28 @@ def run_config3(args, ca, ctx, dev, stream):
     order_ms, quad_ms, lane_ms, total_ms = (parts[k] / nb for k in (1, 2, 3, 4))
     hashed = int(lens.astype("int64").sum())
     algo = hashed + 32 * n
+    # the same batch through the bounds-checked entry point (descriptors from
+    # untrusted data: one more pass over them, include/ciruela_blockhash.h
+    # cir_hash_blocks_dev_bounded), timed the same way: what the check costs
+    out_b = torch.empty_like(out)
+    nrange = torch.full((1,), -1, dtype=torch.int32, device=dev)
+
+    def step_bounded():
+        ca._n.check(lib.cir_hash_blocks_dev_bounded(
+            ctx.handle, 1, data.data_ptr(), nbytes, d_off.data_ptr(), d_len.data_ptr(), n,
+            out_b.data_ptr(), nrange.data_ptr(), stream))
+    for _ in range(args.warmup):
+        step_bounded()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step_bounded()
+    torch.cuda.synchronize()
+    dt_b = (time.perf_counter() - t0) / args.steps
+    bounded = {"ms_per_step": round(dt_b * 1e3, 3), "value": round(hashed / dt_b / GIB, 3),
+               "overhead_pct": round((dt_b / dt - 1) * 100, 2),
+               "out_of_range": int(nrange.item()), "same_digests": bool(torch.equal(out, out_b))}
+    del out_b
     got = out.cpu().numpy().reshape(-1, 32)
     del data, out
     torch.cuda.empty_cache()
@@ -495,6 +517,7 @@ def run_config3(args, ca, ctx, dev, stream):
             "config": {"workload": "config3: 10 GiB of 4 KiB / 32 KiB / 1 MiB blocks (equal bytes "
                                    "per class), 10 % ragged, shuffled, device-resident"},
             "matches_oracle": matches, "oracle_checked_blocks": k,
+            "bounded": bounded,
             "roofline": {
                 "bound": "hbm", "achieved": round(algo / (total_ms / 1e3) / 1e9, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
