@@ -1439,6 +1439,29 @@ def random_case(gpu, ctx, oracle, seed):
     oracle.oracle_hash_blocks(host.ctypes.data, ao.ctypes.data, al.ctypes.data, n,
                               want.ctypes.data, 8)
     assert first_bad(out.cpu().numpy(), want) is None
+    # the same batch through the bounds-checked entry point (the arena is
+    # exactly [0, pos)), with a few descriptors moved out of range (drawn
+    # apart from rng, so the other draws of a seed stay as they were)
+    brng = random.Random(seed ^ 0xB0B0)
+    bad = sorted(brng.sample(range(n), brng.randrange(0, min(n, 12) + 1)))
+    b_off, b_len = list(offs), list(lens)
+    for b in bad:
+        b_off[b], b_len[b] = brng.choice([
+            (pos - b_len[b] + 1, b_len[b]) if b_len[b] else (pos + 1, 0),  # just past the end
+            ((1 << 64) - brng.randrange(1, 1 << 20), brng.randrange(1 << 20, 1 << 21)),  # wraps
+            (brng.randrange(pos + 1, 1 << 50), brng.randrange(0, 70000))])  # far outside
+    d_off = torch.tensor(np.array(b_off, dtype=np.uint64).view(np.int64), device="cuda:0")
+    d_len = torch.tensor(np.array(b_len, dtype=np.uint32).view(np.int32), device="cuda:0")
+    out.fill_(0x5A)
+    nrange = torch.full((1,), -1, dtype=torch.int32, device="cuda:0")
+    gpu._n.check(gpu._n.lib.cir_hash_blocks_dev_bounded(
+        ctx.handle if brng.random() < 0.7 else None, 1, data.data_ptr(), pos, d_off.data_ptr(),
+        d_len.data_ptr(), n, out.data_ptr(), nrange.data_ptr(), None))
+    torch.cuda.synchronize()
+    want = want.reshape(-1, 32)
+    want[bad] = 0
+    assert first_bad(out.cpu().numpy(), want.reshape(-1)) is None
+    assert int(nrange.item()) == len(bad)
     del data, d_off, d_len, out
     # device-resident file
     bs = rng.choice([128 * rng.randrange(1, 64), rng.randrange(100, 9000)])
