@@ -197,6 +197,26 @@ class Context:
         del keep
         return [b == 1 for b in ok.raw]
 
+    def verify_blocks_bounded(self, arena, offsets, lengths, expected, hash_type=None):
+        """verify_blocks for descriptors from untrusted data: nothing is
+        checked here; a block outside the arena is not read and is False."""
+        ht = (hash_type or HashType.blake2b_256()).code
+        n = len(offsets)
+        if len(lengths) != n or len(expected) != 32 * n:
+            raise ValueError("offsets, lengths and expected digests disagree in length")
+        if n == 0:
+            return []
+        offs = (ctypes.c_uint64 * n)(*offsets)
+        lens = (ctypes.c_uint32 * n)(*lengths)
+        ptr, keep = _buf(arena) if len(arena) else (None, None)
+        exp = ctypes.create_string_buffer(bytes(expected), 32 * n)
+        ok = ctypes.create_string_buffer(n)
+        nbad = ctypes.c_size_t()
+        _n.check(_n.lib.cir_verify_blocks_bounded(self._h, ht, ptr, len(arena), offs, lens, n, exp,
+                                                  ok, ctypes.byref(nbad)))
+        del keep
+        return [b == 1 for b in ok.raw]
+
     def verify_blocks_dev(self, d_arena, d_off, d_len, nblk, d_expected, d_digests, d_ok=0,
                           d_nbad=0, stream=0, hash_type=None):
         ht = (hash_type or HashType.blake2b_256()).code

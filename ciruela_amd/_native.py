@@ -114,6 +114,10 @@ _SIGS = {
                                              c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cir_verify_blocks": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, c_vp, c_vp, ctypes.c_size_t,
                                          c_vp, c_vp, c_sizep]),
+    "cir_hash_blocks_bounded": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, ctypes.c_uint64, c_vp,
+                                               c_vp, ctypes.c_size_t, c_vp, c_sizep]),
+    "cir_verify_blocks_bounded": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, ctypes.c_uint64, c_vp,
+                                                 c_vp, ctypes.c_size_t, c_vp, c_vp, c_sizep]),
     "cir_hash_blocks_dev_bounded": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, ctypes.c_uint64, c_vp,
                                                    c_vp, ctypes.c_size_t, c_vp, c_vp, c_vp]),
     "cir_verify_blocks_dev_bounded": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, ctypes.c_uint64,

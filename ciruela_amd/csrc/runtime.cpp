@@ -1604,6 +1604,83 @@ int cir_verify_blocks(cir_ctx* ctx, int hash_type, const uint8_t* h_arena, const
   return CIR_OK;
 } CIR_CATCH_BOUNDARY
 
+// Host descriptors the caller cannot vouch for (the host twins of the
+// *_dev_bounded calls): block b is out of range when off[b] + len[b] wraps
+// or passes arena_bytes.  Such a block is never read (it is hashed as the
+// empty input from the arena's start, then its digest is zeroed); the batch
+// is otherwise the plain call's.  Returns the number flagged, with flag[b]
+// set, or 0 with nothing copied when every block is in range.
+static size_t host_bounds(const uint64_t* off, const uint32_t* len, size_t n,
+                          uint64_t arena_bytes, std::vector<uint64_t>& off2,
+                          std::vector<uint32_t>& len2, std::vector<uint8_t>& flag) {
+  auto out_of_range = [&](size_t b) {
+    const uint64_t end = off[b] + len[b];
+    return end < off[b] || end > arena_bytes;
+  };
+  size_t nflag = 0;
+  for (size_t b = 0; b < n; ++b) nflag += out_of_range(b);
+  if (nflag == 0) return 0;
+  off2.assign(off, off + n);
+  len2.assign(len, len + n);
+  flag.assign(n, 0);
+  for (size_t b = 0; b < n; ++b)
+    if (out_of_range(b)) {
+      flag[b] = 1;
+      off2[b] = 0;
+      len2[b] = 0;
+    }
+  return nflag;
+}
+
+int cir_hash_blocks_bounded(cir_ctx* ctx, int hash_type, const uint8_t* h_arena,
+                            uint64_t arena_bytes, const uint64_t* off, const uint32_t* len,
+                            size_t nblk, uint8_t* h_out, size_t* nrange_out) try {
+  if (nrange_out) *nrange_out = 0;
+  if (nblk && (!off || !len || !h_out)) return fail(CIR_EINVAL, "null pointer");
+  if (nblk && !h_arena && arena_bytes) return fail(CIR_EINVAL, "null arena with arena_bytes > 0");
+  std::vector<uint64_t> off2;
+  std::vector<uint32_t> len2;
+  std::vector<uint8_t> flag;
+  const size_t nflag = host_bounds(off, len, nblk, arena_bytes, off2, len2, flag);
+  static const uint8_t kEmpty = 0;
+  const uint8_t* arena = h_arena ? h_arena : &kEmpty;
+  const int rc = nflag ? cir_hash_blocks_ht(ctx, hash_type, arena, off2.data(), len2.data(), nblk,
+                                            h_out)
+                       : cir_hash_blocks_ht(ctx, hash_type, arena, off, len, nblk, h_out);
+  if (rc) return rc;
+  for (size_t b = 0; nflag && b < nblk; ++b)
+    if (flag[b]) memset(h_out + 32 * b, 0, 32);
+  if (nrange_out) *nrange_out = nflag;
+  return CIR_OK;
+} CIR_CATCH_BOUNDARY
+
+int cir_verify_blocks_bounded(cir_ctx* ctx, int hash_type, const uint8_t* h_arena,
+                              uint64_t arena_bytes, const uint64_t* off, const uint32_t* len,
+                              size_t nblk, const uint8_t* expected, uint8_t* ok_out,
+                              size_t* nbad_out) try {
+  if (nblk && !expected) return fail(CIR_EINVAL, "null pointer");
+  std::vector<uint8_t> got(nblk * 32);
+  size_t nrange = 0;
+  int rc = cir_hash_blocks_bounded(ctx, hash_type, h_arena, arena_bytes, off, len, nblk,
+                                   got.data(), &nrange);
+  if (rc) return rc;
+  // an out-of-range block is a mismatch whatever its expected digest (its
+  // zeroed digest must not match an all-zero expected one)
+  std::vector<uint64_t> off2;
+  std::vector<uint32_t> len2;
+  std::vector<uint8_t> flag;
+  if (nrange) host_bounds(off, len, nblk, arena_bytes, off2, len2, flag);
+  size_t nbad = 0;
+  for (size_t b = 0; b < nblk; ++b) {
+    const bool good =
+        (!nrange || !flag[b]) && memcmp(got.data() + 32 * b, expected + 32 * b, 32) == 0;
+    if (ok_out) ok_out[b] = good ? 1 : 0;
+    nbad += !good;
+  }
+  if (nbad_out) *nbad_out = nbad;
+  return CIR_OK;
+} CIR_CATCH_BOUNDARY
+
 }  // extern "C"
 
 // ---- asynchronous verify (row f2, the daemon's per-block caller) --------

@@ -15,11 +15,11 @@
  *     process on bad input it can check (the reference panics only on
  *     impossible states, e.g. src/block_id.rs:38,41 "length is ok").  The
  *     caller's own buffers are trusted, as a slice is in the reference: the
- *     descriptor batches cir_hash_blocks_dev[_ht] and cir_verify_blocks_dev
+ *     descriptor batches (cir_hash_blocks[_dev][_ht], cir_verify_blocks[_dev])
  *     read arena + off[b] .. + len[b] as given (an out-of-range descriptor is
- *     a GPU memory fault), so descriptors derived from untrusted data go
- *     through the *_dev_bounded entry points, which check every one against
- *     the arena's size on the device.
+ *     a memory fault, on the GPU or the host), so descriptors derived from
+ *     untrusted data go through the *_bounded entry points, which check
+ *     every one against the arena's size (on the device for *_dev_bounded).
  *   - digests are 32 raw bytes (BlockHash([u8; 32]), src/block_id.rs:19),
  *     printed as lowercase hex (src/hexlify.rs:9-13).
  *   - `stream` arguments are hipStream_t passed as void* (NULL = the null
@@ -185,6 +185,16 @@ int cir_hash_blocks_dev_bounded(cir_ctx* ctx, int hash_type, const void* d_arena
 int cir_hash_blocks(cir_ctx* ctx, const uint8_t* h_arena, const uint64_t* off,
                     const uint32_t* len, size_t nblk, uint8_t* h_out);
 
+/* cir_hash_blocks_ht over host descriptors the caller cannot vouch for: the
+ * arena is [h_arena, h_arena + arena_bytes); block b is out of range when
+ * off[b] + len[b] wraps around 2^64 or passes arena_bytes.  Such a block is
+ * never read; its digest is 32 zero bytes and *nrange_out (may be NULL) =
+ * their number.  The other digests are exactly cir_hash_blocks_ht's; with
+ * every block in range nothing is copied (one pass over the descriptors). */
+int cir_hash_blocks_bounded(cir_ctx* ctx, int hash_type, const uint8_t* h_arena,
+                            uint64_t arena_bytes, const uint64_t* off, const uint32_t* len,
+                            size_t nblk, uint8_t* h_out, size_t* nrange_out);
+
 /* dir_signature::v1::Hashes::hash_file(HashType::blake2b_256(), block_size,
  * reader)  (external; call sites src/blocks.rs:193,
  * src/cluster/download.rs:257).  Reads fd from its current offset to EOF.
@@ -243,6 +253,14 @@ int cir_verify_blocks_dev_bounded(cir_ctx* ctx, int hash_type, const void* d_are
 int cir_verify_blocks(cir_ctx* ctx, int hash_type, const uint8_t* h_arena, const uint64_t* off,
                       const uint32_t* len, size_t nblk, const uint8_t* expected, uint8_t* ok_out,
                       size_t* nbad_out);
+
+/* cir_verify_blocks over untrusted host descriptors (checked as
+ * cir_hash_blocks_bounded checks them): an out-of-range block is never read
+ * and is a mismatch (ok_out[b] = 0, counted in *nbad_out). */
+int cir_verify_blocks_bounded(cir_ctx* ctx, int hash_type, const uint8_t* h_arena,
+                              uint64_t arena_bytes, const uint64_t* off, const uint32_t* len,
+                              size_t nblk, const uint8_t* expected, uint8_t* ok_out,
+                              size_t* nbad_out);
 
 /* The same check one block at a time, asynchronously, for a caller that
  * receives blocks one by one (FetchBlock::poll, fetch_blocks.rs:77):

@@ -14,7 +14,7 @@ import random
 import numpy as np
 import pytest
 
-from conftest import oracle_sha
+from conftest import oracle_digest, oracle_sha
 
 pytestmark = pytest.mark.gpu
 
@@ -231,3 +231,52 @@ def test_bounded_empty_and_argument_errors(gpu, ctx):
                                 nrange.data_ptr())
     torch.cuda.synchronize()
     assert int(nrange.item()) == 1 and not out.any()
+
+
+@pytest.mark.parametrize("ht", ["blake2b", "sha512"])
+def test_host_bounded_batches(gpu, oracle, ht):
+    """cir_hash_blocks_bounded / cir_verify_blocks_bounded: the host twins.
+    Out-of-range descriptors (the same kinds) are never read -- one of 2^40
+    past a 3 MiB arena would fault the process -- their digests are zeros
+    and they fail verification; the rest equal the oracle's.  Through a
+    context with two device states (the split host path) too."""
+    import ctypes
+    from ciruela_amd import _native as n
+    hasht = gpu.HashType.blake2b_256() if ht == "blake2b" else gpu.HashType.sha512_256()
+    dig = (lambda d: oracle_digest(oracle, d)) if ht == "blake2b" else \
+        (lambda d: oracle_sha(oracle, d))
+    rng = random.Random(91 + len(ht))
+    arena_bytes = 3 << 20
+    arena = rng.randbytes(arena_bytes)
+    offs, lens = _batch(rng, 500, arena_bytes, 60 if ht == "blake2b" else 0)
+    for j, (o, ln) in enumerate(_edges_in_range(arena_bytes)):
+        offs[j + 1], lens[j + 1] = o, ln
+    bad = _poison(rng, offs, lens, arena_bytes, 9)
+    want = [bytes(32) if i in bad else dig(arena[o:o + ln])
+            for i, (o, ln) in enumerate(zip(offs, lens))]
+    for split in ("1", "2"):
+        import os
+        os.environ["CIR_DEBUG_SPLIT"] = split
+        try:
+            c = gpu.Context(device_mask=1, staging_bytes=1 << 20)
+        finally:
+            del os.environ["CIR_DEBUG_SPLIT"]
+        k = len(offs)
+        ao = (ctypes.c_uint64 * k)(*offs)
+        al = (ctypes.c_uint32 * k)(*lens)
+        buf = ctypes.create_string_buffer(arena, arena_bytes)
+        out = ctypes.create_string_buffer(32 * k)
+        nrange = ctypes.c_size_t(77)
+        n.check(n.lib.cir_hash_blocks_bounded(c.handle, hasht.code, buf, arena_bytes, ao, al, k,
+                                              out, ctypes.byref(nrange)))
+        got = [out.raw[32 * i:32 * i + 32] for i in range(k)]
+        assert [i for i in range(k) if got[i] != want[i]] == []
+        assert nrange.value == len(bad)
+        # verify: expected = the true digests of the original blocks (as a
+        # peer would claim), one corrupted, one out-of-range block expecting
+        # zeros
+        exp = bytearray(b"".join(want))
+        exp[32 * 5] ^= 1
+        ok = c.verify_blocks_bounded(arena, offs, lens, bytes(exp), hash_type=hasht)
+        assert [i for i, g in enumerate(ok) if not g] == sorted(set(bad) | {5})
+        c.close()

@@ -97,6 +97,32 @@ static void descriptors(cir_ctx* ctx, int ht) {
                           &nbad) == 0);
   CHECK(nbad == bad);
   for (size_t i = 0; i < n; ++i) CHECK(ok[i] == (i % 7 != 0));
+  // the bounded host twins, two descriptors moved out of the arena (past its
+  // end; wrapping around 2^64): never read, zero digests, failed
+  {
+    std::vector<uint64_t> boff = off;
+    std::vector<uint32_t> blen = len;
+    const size_t b1 = rng() % n, b2 = (b1 + 1) % n;
+    boff[b1] = arena.size() + 1 - blen[b1];
+    boff[b2] = ~0ull - 3;
+    blen[b2] = 100;
+    const size_t nf = b1 == b2 ? 1 : 2;
+    std::vector<uint8_t> bgot(32 * n);
+    size_t nrange = 0;
+    CHECK(cir_hash_blocks_bounded(ctx, ht, arena.data(), arena.size(), boff.data(), blen.data(), n,
+                                  bgot.data(), &nrange) == 0);
+    CHECK(nrange == nf);
+    for (size_t i = 0; i < n; ++i) {
+      const bool flagged = i == b1 || i == b2;
+      for (int j = 0; j < 32 && flagged; ++j) CHECK(bgot[32 * i + j] == 0);
+      if (!flagged) CHECK(memcmp(&bgot[32 * i], &want[32 * i], 32) == 0);
+    }
+    size_t bbad = 0;
+    CHECK(cir_verify_blocks_bounded(ctx, ht, arena.data(), arena.size(), boff.data(), blen.data(),
+                                    n, want.data(), ok.data(), &bbad) == 0);
+    CHECK(bbad == nf);
+    for (size_t i = 0; i < n; ++i) CHECK(ok[i] == ((i == b1 || i == b2) ? 0 : 1));
+  }
   // the asynchronous verify: some polled, some forgotten, the rest awaited
   const size_t k = std::min<size_t>(n, 64);
   std::vector<uint64_t> t(k);
