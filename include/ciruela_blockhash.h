@@ -24,7 +24,10 @@
  *     printed as lowercase hex (src/hexlify.rs:9-13).
  *   - `stream` arguments are hipStream_t passed as void* (NULL = the null
  *     stream of the calling thread's current device).  *_dev calls are
- *     asynchronous on that stream and never synchronise the device.
+ *     asynchronous on that stream and never synchronise the device (with a
+ *     context, a descriptor batch larger than any before grows the device's
+ *     ordering or bounds scratch, waiting once for that scratch's previous
+ *     user).
  *   - no call changes the calling thread's current HIP device: entry points
  *     that work on other devices restore it before returning.
  *   - buffers returned through `uint8_t**` are released with cir_free().
