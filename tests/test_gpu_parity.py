@@ -2046,6 +2046,29 @@ def random_tree(root, rng, bs):
         os.symlink(rng.choice(["../a", "target %d" % k, "x" * 70]), d / ("l%d" % k))
 
 
+def deep_chain(root, rng, bs):
+    """A chain of directories whose path passes PATH_MAX below root (made
+    through dir fds), with files of a few blocks at some levels: the scan
+    opens such directories relative to their parent's fd and such files
+    piecewise (scan.cpp read_dir, open_long)."""
+    depth = rng.randrange(14, 24)
+    fd = os.open(str(root), os.O_RDONLY | os.O_DIRECTORY)
+    try:
+        for i in range(depth):
+            if rng.random() < 0.3 or i == depth - 1:
+                size = max(0, rng.choice([0, 1, 2, 3]) * bs + rng.randrange(-1, 200))
+                f = os.open("g%02d" % i, os.O_WRONLY | os.O_CREAT, 0o644, dir_fd=fd)
+                os.write(f, rng.randbytes(size))
+                os.close(f)
+            name = ("deep%02d_" % i) + "q" * rng.randrange(200, 240)
+            os.mkdir(name, dir_fd=fd)
+            nfd = os.open(name, os.O_RDONLY | os.O_DIRECTORY, dir_fd=fd)
+            os.close(fd)
+            fd = nfd
+    finally:
+        os.close(fd)
+
+
 def scan_case(gpu, seed, tmp_path, monkeypatch):
     """One randomized end-to-end scan against the scan oracle, over the
     scan's knobs: block size (up to one above the staging size), hash type,
@@ -2060,6 +2083,11 @@ def scan_case(gpu, seed, tmp_path, monkeypatch):
     root = tmp_path / ("t%d" % seed)
     root.mkdir()
     random_tree(root, rng, bs)
+    # one tree in six also holds a chain nested past PATH_MAX (drawn apart
+    # from rng, so the other draws of a seed stay as they were)
+    drng = random.Random(seed ^ 0xDEE9)
+    if drng.random() < 1 / 6:
+        deep_chain(root, drng, bs)
     hash_name = "sha512/256" if rng.random() < 0.2 else "blake2b/256"
     split = rng.choice([1, 1, 2, 3])
     monkeypatch.setenv("CIR_STAGE_COPY", rng.choice(["direct", "nt"]))
